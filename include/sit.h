@@ -1,0 +1,273 @@
+/*
+ * sit.h — C ABI of the MI355X-native ship-in-transit (SIT) environment step.
+ *
+ * This is the drop-in boundary for the one hot path of AndreasKing-Goks/sac-maritime-ast:
+ * the two-ship `MultiShipRLEnv` (RLEnv/MSRL_Env.py:37-450, completed by
+ * RLEnv/MSRL_env_ex.py:450-980) stepping the ship-in-transit simulator
+ * (simulators/ship_in_transit/*.py).  One handle holds N independent two-ship
+ * environments ("envs"): ship type 0 is the ship under test, type 1 the obstacle
+ * ship whose route the AST sampler perturbs with intermediate waypoints (IWs).
+ *
+ * Conventions
+ *  - Plain C types only; no HIP/torch types cross the boundary.  `stream` is a
+ *    hipStream_t passed as void* (NULL = default stream).
+ *  - "real" below means float32 when the handle was created with SIT_F32 and
+ *    float64 with SIT_F64.  Every per-step array argument is a DEVICE pointer
+ *    owned by the caller; setup calls (sit_load_*) take HOST pointers.
+ *  - Every entry point returns SIT_OK (0) or a negative SIT_E_* code; the message
+ *    is available from sit_last_error().  No exception crosses the ABI.
+ *  - Calls are stream-ordered and asynchronous.  A handle must not be used from two
+ *    host threads at once; independent handles (one per GPU/stream) are independent.
+ *
+ * Reference interface each entry point replaces (file:line in the reference):
+ *   sit_create / sit_load_*   MultiShipRLEnv.__init__ + ShipAssets    MSRL_Env.py:25-116,
+ *                             ShipModelAST/ShipMachineryModel/controllers constructors
+ *                             (ship_model.py:563-574, ship_engine.py:298-353,
+ *                              controllers.py:114-136, 253-296), PolygonObstacle obstacle.py:98-124
+ *   sit_reset                 MultiShipRLEnv.reset                    MSRL_Env.py:147-188
+ *   sit_init_step             MultiShipRLEnv.init_step                MSRL_Env.py:190-217
+ *   sit_step                  MultiShipRLEnv.step                     MSRL_Env.py:404-442
+ *                             (+ reward_function                      MSRL_env_ex.py:906-980)
+ *   sit_rollout               K x step with the driver loop of test_beds/main_ast.py:310-412
+ *                             (the consumer ast_core/samplers/intermediate_waypoint_sampler.py
+ *                              is empty in the reference; the synthetic sampler is SURVEY §8(d))
+ *   sit_get_state/set_state   (no reference counterpart: SoA export/import for teacher-forced
+ *                              parity and checkpointing)
+ */
+#ifndef SIT_H
+#define SIT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIT_ABI_VERSION 1
+
+/* ---- return codes ---------------------------------------------------------------- */
+#define SIT_OK 0
+#define SIT_E_INVALID (-1)   /* bad argument (null pointer, out-of-range size, ...) */
+#define SIT_E_HIP (-2)       /* a HIP runtime call failed */
+#define SIT_E_NOMEM (-3)     /* device allocation failed */
+#define SIT_E_STATE (-4)     /* call out of order (e.g. stepping before routes are loaded) */
+
+/* ---- precision of a handle -------------------------------------------------------- */
+#define SIT_F32 32
+#define SIT_F64 64
+
+/* ---- hybrid shaft generator state (ship_engine.py:32-76) --------------------------- */
+#define SIT_SG_MOTOR 0 /* 'MOTOR' (PTI)  */
+#define SIT_SG_GEN 1   /* 'GEN'   (PTO)  */
+#define SIT_SG_OFF 2   /* anything else  */
+
+/* ---- status bitmask: one bit per reference status string, in the order the
+ *      reference concatenates them (MSRL_env_ex.py:755-803, 830-874, 897-899) ------- */
+#define SIT_ST_TEST_ENDPOINT (1u << 0)   /* "|Test ship reaches endpoint|"             */
+#define SIT_ST_TEST_HORIZON (1u << 1)    /* "|Test ship hits map horizon|"             */
+#define SIT_ST_TEST_TERRAIN (1u << 2)    /* "|Test ship collides with the terrain|"    */
+#define SIT_ST_TEST_MECHANICAL (1u << 3) /* "|Test ship mechanical failure|"           */
+#define SIT_ST_TEST_NAVIGATION (1u << 4) /* "|Test ship navigation failure|"           */
+#define SIT_ST_TEST_BLACKOUT (1u << 5)   /* "|Test ship blackout failure|"             */
+#define SIT_ST_OBS_ENDPOINT (1u << 6)    /* "|Obstacle ship reaches endpoint|"         */
+#define SIT_ST_OBS_HORIZON (1u << 7)     /* "|Obstacle ship hits map horizon|"         */
+#define SIT_ST_OBS_TERRAIN (1u << 8)     /* "|Obstacle ship collides with the terrain|"*/
+#define SIT_ST_OBS_IW_TERMINAL (1u << 9) /* "|Obstacle ship IW sampled in terminal state|" */
+#define SIT_ST_OBS_NAVIGATION (1u << 10) /* "|Obstacle ship navigation failure|"       */
+#define SIT_ST_COLLISION (1u << 11)      /* "|Ship collision|"                         */
+#define SIT_ST_TEST_DONE (1u << 12)      /* test ship terminal  (else "|Test ship not in terminal state|")     */
+#define SIT_ST_OBS_DONE (1u << 13)       /* obstacle ship terminal (else "|Obstacle ship not in terminal state|") */
+#define SIT_ST_ROUTE_OVERFLOW (1u << 31) /* IW insertion dropped: route table full (no reference counterpart) */
+
+/* ---- next_state layout (MSRL_Env.py:426-437) --------------------------------------- */
+#define SIT_OBS_DIM 10 /* test n,e,psi,rpm,|e_ct|,P_me[kW], obs n,e,psi,|e_ct| */
+
+/* ---- per-ship initial values for sit_load_initial ---------------------------------- */
+enum {
+  SIT_INIT_NORTH = 0,      /* SimulationConfiguration.initial_north_position_m           */
+  SIT_INIT_EAST,           /* initial_east_position_m                                    */
+  SIT_INIT_YAW,            /* initial_yaw_angle_rad                                      */
+  SIT_INIT_SURGE,          /* initial_forward_speed_m_per_s                              */
+  SIT_INIT_SWAY,           /* initial_sideways_speed_m_per_s                             */
+  SIT_INIT_YAW_RATE,       /* initial_yaw_rate_rad_per_s                                 */
+  SIT_INIT_SHAFT_SPEED,    /* initial_propeller_shaft_speed_rad_per_s (ship_model.py:567) */
+  SIT_INIT_DESIRED_SPEED,  /* ShipAssets.desired_forward_speed (MSRL_Env.py:30)           */
+  SIT_INIT_SHIP_SPEED_I,   /* ship-speed PI initial integral (controllers.py:122-124: 0)  */
+  SIT_INIT_SHAFT_SPEED_I,  /* initial_shaft_speed_integral_error (controllers.py:119, 129) */
+  SIT_INIT_NF
+};
+
+/* ---- configuration: the reference's NamedTuple fields, verbatim ------------------- */
+typedef struct sit_params {
+  /* ShipConfiguration (ship_model.py:20-35) */
+  double dead_weight_tonnage;
+  double coefficient_of_deadweight_to_displacement;
+  double bunkers;
+  double ballast;
+  double length_of_ship;
+  double width_of_ship;
+  double added_mass_coefficient_in_surge;
+  double added_mass_coefficient_in_sway;
+  double added_mass_coefficient_in_yaw;
+  double mass_over_linear_friction_coefficient_in_surge;
+  double mass_over_linear_friction_coefficient_in_sway;
+  double mass_over_linear_friction_coefficient_in_yaw;
+  double nonlinear_friction_coefficient_in_surge;
+  double nonlinear_friction_coefficient_in_sway;
+  double nonlinear_friction_coefficient_in_yaw;
+  /* EnvironmentConfiguration (ship_model.py:38-42) */
+  double current_velocity_component_from_north;
+  double current_velocity_component_from_east;
+  double wind_speed;
+  double wind_direction;
+  /* wind model constants hard-coded in BaseShipModel (ship_model.py:123-130) */
+  double rho_air;
+  double front_height;
+  double side_height;
+  double cx;
+  double cy;
+  double cn;
+  /* SimulationConfiguration.integration_step (ship_model.py:52) */
+  double integration_step;
+  /* MachinerySystemConfiguration (ship_engine.py:121-138) and the selected MachineryMode */
+  double hotel_load;
+  double main_engine_capacity;   /* MachineryModeParams of the operating mode */
+  double electrical_capacity;
+  int32_t shaft_generator_state; /* SIT_SG_* */
+  int32_t _pad0;
+  double rated_speed_main_engine_rpm;
+  double linear_friction_main_engine;
+  double linear_friction_hybrid_shaft_generator;
+  double gear_ratio_between_main_engine_and_propeller;
+  double gear_ratio_between_hybrid_shaft_generator_and_propeller;
+  double propeller_inertia;
+  double propeller_speed_to_torque_coefficient;
+  double propeller_diameter;
+  double propeller_speed_to_thrust_force_coefficient;
+  double rudder_angle_to_sway_force_coefficient;
+  double rudder_angle_to_yaw_force_coefficient;
+  double max_rudder_angle_degrees;
+  /* ThrottleControllerGains (controllers.py:16-20) */
+  double kp_ship_speed;
+  double ki_ship_speed;
+  double kp_shaft_speed;
+  double ki_shaft_speed;
+  /* HeadingControllerGains (controllers.py:23-26) */
+  double heading_kp;
+  double heading_kd;
+  double heading_ki;
+  /* LosParameters (LOS_guidance.py:15-19) */
+  double radius_of_acceptance;
+  double lookahead_distance;
+  double los_integral_gain;
+  double integrator_windup_limit;
+  /* env args (test_policy.py:39-42) and reward constants of MSRL_env_ex.py */
+  double theta;                  /* navigation-failure coefficient (:569)      */
+  int32_t sampling_frequency;    /* AB segment divisor (:125)                  */
+  int32_t collision_bias;        /* 1 = reference behaviour: always on (MSRL_Env.py:98-99, 242) */
+  double e_tolerance;            /* 1000 (:119)                                */
+  double arrival_radius;         /* 200  (:754, :829)                          */
+  double shaft_rpm_max;          /* 2000 (:557)                                */
+  double minimum_ship_distance;  /* 50   (:592)                                */
+  double bias_throttle_scale;    /* 0.5  (MSRL_Env.py:246)                     */
+  double bias_throttle_max;      /* 1.1  (MSRL_Env.py:247)                     */
+  double bias_rudder_degrees;    /* 3    (MSRL_Env.py:250)                     */
+} sit_params;
+
+/* Fill `p` with the configuration of test_beds/test_policy.py:94-226 (PTI mode). */
+void sit_params_default(sit_params* p);
+
+/* ---- handle lifecycle ------------------------------------------------------------- */
+typedef struct sit_handle sit_handle;
+
+/* Create N envs on the current HIP device.  `wpt_capacity` bounds the waypoints of one
+ * ship's route including start and end (IW insertions beyond it set
+ * SIT_ST_ROUTE_OVERFLOW and are dropped).  `precision` is SIT_F32 or SIT_F64. */
+int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t precision,
+               sit_handle** out);
+void sit_destroy(sit_handle* h);
+/* Last error message of `h`, or of the failed sit_create on this thread when h == NULL. */
+const char* sit_last_error(const sit_handle* h);
+int32_t sit_abi_version(void);
+int32_t sit_precision(const sit_handle* h);
+int32_t sit_n_env(const sit_handle* h);
+
+/* ---- setup (host pointers) --------------------------------------------------------- */
+/* Island map: PolygonObstacle(list_of_vertices_list) (obstacle.py:98-124).  Vertices are
+ * (east, north) pairs exactly as in the reference; polygon p owns vertices
+ * [vert_offsets[p], vert_offsets[p+1]).  The ring is closed implicitly. */
+int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets,
+                 const double* verts_en);
+/* Routes: wpt_ne[env][ship][i][2] = (north, east) for i < n_wpt[env][ship], laid out with
+ * stride wpt_capacity in i (NavigationSystem.load_waypoints, LOS_guidance.py:65-86). */
+int sit_load_routes(sit_handle* h, const double* wpt_ne, const int32_t* n_wpt);
+/* Construction-time values: init[env][ship][SIT_INIT_NF]. */
+int sit_load_initial(sit_handle* h, const double* init);
+/* Put every env into its construction-time state (as if freshly built).  Unlike
+ * sit_reset this also re-initialises the shaft speed and all controller integrators. */
+int sit_restart(sit_handle* h, void* stream);
+
+/* ---- stepping (device pointers, stream-ordered) ------------------------------------ */
+/* MultiShipRLEnv.reset for envs with env_mask[e] != 0 (NULL = all).  Keeps shaft speed and
+ * all PI/PID integrator states, as the reference does.  If initial_state is not NULL it
+ * receives the construction-time observation, real[n_env][SIT_OBS_DIM]. */
+int sit_reset(sit_handle* h, const uint8_t* env_mask, void* initial_state, void* stream);
+/* MultiShipRLEnv.init_step for masked envs (NULL = all). */
+int sit_init_step(sit_handle* h, const uint8_t* env_mask, void* stream);
+/* MultiShipRLEnv.step for all envs.
+ *   action_ne  real[n_env][2]  converted_action = intermediate waypoint (north, east)
+ *   sac_update u8[n_env]       SAC_update: insert the IW into the obstacle ship's route
+ *   init       u8[n_env]       init: first step of an episode (no distance accounting)
+ *   next_state real[n_env][SIT_OBS_DIM], reward real[n_env], done u8[n_env], status u32[n_env]
+ *   done_count int32[1] or NULL: += number of envs with done (wave ballot reduction) */
+int sit_step(sit_handle* h, const void* action_ne, const uint8_t* sac_update,
+             const uint8_t* init, void* next_state, void* reward, uint8_t* done,
+             uint32_t* status, int32_t* done_count, void* stream);
+
+/* K fused steps.  With action_ne == NULL the synthetic AST sampler drives the obstacle
+ * ship: a sampling event happens on the first step of an episode and
+ * whenever the obstacle ship's sampling distance reaches AB_len; it draws
+ * a ~ U[-pi/6, pi/6] from Philox4x32-10(key = seed, counter = (env_id, event, 0x5A4D, 0))
+ * and inserts IW = (n + AB_len cos(AB_alpha + a), e + AB_len sin(AB_alpha + a)).
+ * Otherwise action_ne/sac_update/init are [n_steps][n_env] explicit inputs.
+ * With auto_reset != 0, an env whose step returned done is reset, init-stepped and
+ * restarted at episode step 1 before its next step (test_beds/main_ast.py:310-330).
+ * Output arrays are [n_steps][n_env]...; any may be NULL except that at least one of
+ * next_state/reward must be given.  action_out (real[n_steps][n_env][4]) receives
+ * (IW north, IW east, scoping angle a, SAC_update) of every step. */
+typedef struct sit_rollout_args {
+  int32_t n_steps;
+  int32_t auto_reset;
+  uint64_t seed;
+  int64_t env_id_offset;     /* global id of env 0 (for sharding across GPUs) */
+  const void* action_ne;     /* real[n_steps][n_env][2] or NULL (synthetic sampler) */
+  const uint8_t* sac_update; /* u8[n_steps][n_env] (explicit mode only) */
+  const uint8_t* init;       /* u8[n_steps][n_env] (explicit mode only) */
+  void* next_state;          /* real[n_steps][n_env][SIT_OBS_DIM] or NULL */
+  void* reward;              /* real[n_steps][n_env] or NULL */
+  uint8_t* done;             /* u8[n_steps][n_env] or NULL */
+  uint32_t* status;          /* u32[n_steps][n_env] or NULL */
+  void* action_out;          /* real[n_steps][n_env][4] or NULL */
+  int32_t* done_count;       /* int32[n_steps] or NULL: += envs done at each step */
+} sit_rollout_args;
+int sit_rollout(sit_handle* h, const sit_rollout_args* a, void* stream);
+
+/* ---- state export / import (device blob) ------------------------------------------ */
+/* The dynamic state of all envs (ship states, controller integrators, route tables,
+ * stop flags, counters) lives in one device blob; fields are described by
+ * sit_state_field(id) for id in [0, sit_state_nfields()). */
+#define SIT_DT_REAL 0
+#define SIT_DT_I32 1
+#define SIT_DT_U32 2
+int32_t sit_state_nfields(void);
+int sit_state_field(const sit_handle* h, int32_t id, const char** name, size_t* offset,
+                    int32_t* dtype, int64_t* count);
+int sit_state_bytes(const sit_handle* h, size_t* bytes);
+int sit_get_state(sit_handle* h, void* dst, void* stream);
+int sit_set_state(sit_handle* h, const void* src, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIT_H */

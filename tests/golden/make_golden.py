@@ -1,0 +1,591 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures by running the REFERENCE itself.
+
+Run ONLY in the build container (the reference is absent on the GPU box):
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+
+The reference (AndreasKing-Goks/sac-maritime-ast @ 2025-06-29) is imported read-only from
+$SIT_REFERENCE (default /root/reference) with bytecode writing disabled.  Nothing of the
+reference is copied into this repository: only the numbers it produces are saved.
+
+* ``sim_*.npz`` — the simulator core (simulators/ship_in_transit/*.py) imports and runs
+  unmodified.  One ship, driven exactly like MSRL_Env.obs_step's non-stop path
+  (MSRL_Env.py:347-375) or test_step with the collision bias (MSRL_Env.py:223-262).
+* ``env_*.npz`` — the env layer RLEnv/MSRL_env_ex.py (the complete MultiShipRLEnv with
+  reward_function, MSRL_env_ex.py:450-980) needs gymnasium, shapely and a package named
+  ``simulator``, none of which exist here.  It is run under harness shims: a gymnasium API
+  stub (Env/Box/seeding, no arithmetic), ``simulator.*`` module aliases to
+  ``simulators.ship_in_transit.*``, and a shapely.geometry stand-in whose Polygon.contains
+  uses matplotlib.path and whose exterior.distance is the textbook clamp-projection segment
+  distance.  Everything except those two polygon predicates is the reference's own code, so
+  the env fixtures pin reward ordering, stop flags, status strings, the stop path, distance
+  accounting and route insertion; polygon predicates stay *parity-unpinned* against real
+  shapely (not installed, not pinned by the reference's env files).
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import math
+import os
+import sys
+import types
+from types import SimpleNamespace
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.environ.get("SIT_REFERENCE", "/root/reference")
+sys.dont_write_bytecode = True
+os.environ.setdefault("MPLBACKEND", "Agg")
+
+# ---------------------------------------------------------------------------------
+# scenario; map = test_beds/test_policy.py:189-194 (east, north) vertices
+# ---------------------------------------------------------------------------------
+R_TEST = [[1200.0, 500.0], [1500.0, 4500.0], [3500.0, 7000.0], [7000.0, 9000.0], [9500.0, 9000.0]]
+R_OBS = [[2200.0, 5300.0], [8600.0, 5200.0]]
+MAP = [
+    [(0, 10000), (5500, 10000), (5300, 9000), (4800, 8500), (4200, 7300), (4000, 5700), (4300, 4900),
+     (4900, 4400), (4400, 4000), (3200, 4100), (2000, 4500), (1000, 4000), (900, 3500), (500, 2600),
+     (0, 2350)],
+    [(10000, 0), (4000, 0), (4250, 250), (5000, 400), (6000, 900), (8000, 1100), (8500, 1500),
+     (9000, 2250), (9500, 3500), (10000, 4000)],
+    [(5500, 5500), (5700, 7000), (6200, 8100), (7500, 8000), (7800, 7000), (7600, 5500), (6900, 4700),
+     (6000, 5000)],
+    [(2000, 2000), (2500, 2300), (4000, 2500), (5000, 3000), (4200, 2100), (3400, 1900)],
+]
+CAP = 40
+DT = 0.5
+OMEGA0 = 400 * np.pi / 30
+V_DES = 8.5
+
+
+def _import_reference():
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from simulators.ship_in_transit import controllers, LOS_guidance, ship_engine, ship_model  # noqa
+    return SimpleNamespace(sm=ship_model, se=ship_engine, ctl=controllers, los=LOS_guidance)
+
+
+def install_env_shims():
+    """gymnasium API stub, shapely stand-in, simulator.* aliases (see module docstring)."""
+    gym = types.ModuleType("gymnasium")
+    spaces = types.ModuleType("gymnasium.spaces")
+    utils = types.ModuleType("gymnasium.utils")
+    seeding = types.ModuleType("gymnasium.utils.seeding")
+
+    class Env:
+        def __init__(self, *a, **k):
+            pass
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32, **k):
+            self.low, self.high = np.asarray(low), np.asarray(high)
+            self.shape = self.low.shape
+
+        def seed(self, seed=None):
+            return [seed]
+
+    seeding.np_random = lambda seed=None: (np.random.default_rng(seed), seed)
+    gym.Env, spaces.Box, utils.seeding = Env, Box, seeding
+    gym.spaces, gym.utils = spaces, utils
+    sys.modules.update({"gymnasium": gym, "gymnasium.spaces": spaces, "gymnasium.utils": utils,
+                        "gymnasium.utils.seeding": seeding})
+
+    import matplotlib.path as mpath
+
+    shp = types.ModuleType("shapely")
+    geom = types.ModuleType("shapely.geometry")
+
+    class Point:
+        def __init__(self, x, y):
+            self.x, self.y = float(x), float(y)
+
+    class _Ring:
+        def __init__(self, verts):
+            self.v = [(float(x), float(y)) for x, y in verts]
+            if self.v[0] != self.v[-1]:
+                self.v.append(self.v[0])
+
+        def distance(self, p):
+            best = math.inf
+            for (ax, ay), (bx, by) in zip(self.v[:-1], self.v[1:]):
+                dx, dy = bx - ax, by - ay
+                l2 = dx * dx + dy * dy
+                t = 0.0 if l2 == 0 else max(0.0, min(1.0, ((p.x - ax) * dx + (p.y - ay) * dy) / l2))
+                best = min(best, math.hypot(p.x - (ax + t * dx), p.y - (ay + t * dy)))
+            return best
+
+    class Polygon:
+        def __init__(self, verts):
+            self.exterior = _Ring(verts)
+            self._path = mpath.Path(np.asarray(self.exterior.v))
+
+        def contains(self, p):
+            return bool(self._path.contains_point((p.x, p.y)))
+
+    geom.Point, geom.Polygon = Point, Polygon
+    shp.geometry = geom
+    sys.modules.update({"shapely": shp, "shapely.geometry": geom})
+
+    ref = _import_reference()
+    from simulators.ship_in_transit import obstacle  # noqa: E402  (needs the stand-in)
+    sim = types.ModuleType("simulator")
+    sys.modules.update({"simulator": sim, "simulator.ship_model": ref.sm,
+                        "simulator.controllers": ref.ctl, "simulator.obstacle": obstacle})
+    import importlib
+    env_mod = importlib.import_module("RLEnv.MSRL_env_ex")
+    return ref, obstacle, env_mod
+
+
+# ---------------------------------------------------------------------------------
+# reference object construction (test_beds/test_policy.py:94-226)
+# ---------------------------------------------------------------------------------
+# machinery operating modes of test_beds/test_policy.py:125-144 (PTI is the one configured)
+MODES = {"PTI": ("MOTOR", 0.0, 2 * 510e3), "PTO": ("GEN", 2160e3, 0.0), "MEC": ("OFF", 2160e3, 510e3)}
+MODE_ID = {"MOTOR": 0, "GEN": 1, "OFF": 2}
+
+
+def build_ship(ref, route, pose, v_des=V_DES, omega0=OMEGA0, pi2=114.0, mode="PTI"):
+    sm, se, ctl, los = ref.sm, ref.se, ref.ctl, ref.los
+    sg, me_cap, el_cap = MODES[mode]
+    ship_config = sm.ShipConfiguration(
+        coefficient_of_deadweight_to_displacement=0.7, bunkers=200000, ballast=200000,
+        length_of_ship=80, width_of_ship=16, added_mass_coefficient_in_surge=0.4,
+        added_mass_coefficient_in_sway=0.4, added_mass_coefficient_in_yaw=0.4,
+        dead_weight_tonnage=3850000, mass_over_linear_friction_coefficient_in_surge=130,
+        mass_over_linear_friction_coefficient_in_sway=18, mass_over_linear_friction_coefficient_in_yaw=90,
+        nonlinear_friction_coefficient__in_surge=2400, nonlinear_friction_coefficient__in_sway=4000,
+        nonlinear_friction_coefficient__in_yaw=400)
+    env_config = sm.EnvironmentConfiguration(current_velocity_component_from_north=-2,
+                                             current_velocity_component_from_east=-2,
+                                             wind_speed=2, wind_direction=-np.pi / 4)
+    pti = se.MachineryMode(params=se.MachineryModeParams(main_engine_capacity=me_cap,
+                                                         electrical_capacity=el_cap,
+                                                         shaft_generator_state=sg))
+    machinery_config = se.MachinerySystemConfiguration(
+        machinery_modes=se.MachineryModes([pti]), machinery_operating_mode=0,
+        linear_friction_main_engine=68, linear_friction_hybrid_shaft_generator=57,
+        gear_ratio_between_main_engine_and_propeller=0.6,
+        gear_ratio_between_hybrid_shaft_generator_and_propeller=0.6, propeller_inertia=6000,
+        propeller_diameter=3.1, propeller_speed_to_torque_coefficient=7.5,
+        propeller_speed_to_thrust_force_coefficient=1.7, hotel_load=200000,
+        rated_speed_main_engine_rpm=1000, rudder_angle_to_sway_force_coefficient=50e3,
+        rudder_angle_to_yaw_force_coefficient=500e3, max_rudder_angle_degrees=30,
+        specific_fuel_consumption_coefficients_me=se.SpecificFuelConsumptionWartila6L26().fuel_consumption_coefficients(),
+        specific_fuel_consumption_coefficients_dg=se.SpecificFuelConsumptionBaudouin6M26Dot3().fuel_consumption_coefficients())
+    sim = sm.SimulationConfiguration(initial_north_position_m=pose[0], initial_east_position_m=pose[1],
+                                     initial_yaw_angle_rad=pose[2], initial_forward_speed_m_per_s=pose[3],
+                                     initial_sideways_speed_m_per_s=pose[4], initial_yaw_rate_rad_per_s=pose[5],
+                                     integration_step=DT, simulation_time=3600)
+    ship = sm.ShipModelAST(ship_config=ship_config, machinery_config=machinery_config,
+                           environment_config=env_config, simulation_config=sim,
+                           initial_propeller_shaft_speed_rad_per_s=omega0)
+    thr = ctl.EngineThrottleFromSpeedSetPoint(
+        gains=ctl.ThrottleControllerGains(kp_ship_speed=7, ki_ship_speed=0.13, kp_shaft_speed=0.05,
+                                          ki_shaft_speed=0.005),
+        max_shaft_speed=ship.ship_machinery_model.shaft_speed_max, time_step=DT,
+        initial_shaft_speed_integral_error=pi2)
+    ap = ctl.HeadingBySampledRouteController(
+        [list(p) for p in route], heading_controller_gains=ctl.HeadingControllerGains(kp=1, kd=90, ki=0.01),
+        los_parameters=los.LosParameters(radius_of_acceptance=300, lookahead_distance=1000,
+                                         integral_gain=0.002, integrator_windup_limit=4000),
+        time_step=DT, max_rudder_angle=30 * np.pi / 180, num_of_samplings=2)
+    return ship, thr, ap
+
+
+def ship_snapshot(ship, thr, ap):
+    res = ship.simulation_results
+    last = lambda k: res[k][-1] if res[k] else 0.0  # noqa: E731
+    mm = ship.ship_machinery_model
+    pid = ap.heading_controller.ship_heading_controller
+    return dict(north=ship.north, east=ship.east, yaw=ship.yaw_angle, surge=ship.forward_speed,
+                sway=ship.sideways_speed, yaw_rate=ship.yaw_rate, shaft_speed=mm.omega,
+                ship_speed_i=thr.ship_speed_controller.error_i,
+                shaft_speed_i=thr.shaft_speed_controller.error_i,
+                heading_i=pid.error_i, heading_prev=pid.prev_error, e_ct_int=ap.navigate.e_ct_int,
+                last_rpm=last("propeller shaft speed [rpm]"), last_e_ct=last("cross track error [m]"),
+                last_power_me=last("power me [kw]"), next_wpt=ap.next_wpt,
+                n_wpt=len(ap.navigate.north), ticks=int(round(ship.int.time / DT)))
+
+
+def set_ship(ship, thr, ap, st):
+    ship.north, ship.east, ship.yaw_angle = st["north"], st["east"], st["yaw"]
+    ship.forward_speed, ship.sideways_speed, ship.yaw_rate = st["surge"], st["sway"], st["yaw_rate"]
+    ship.ship_machinery_model.omega = st["shaft_speed"]
+    thr.ship_speed_controller.error_i = st["ship_speed_i"]
+    thr.shaft_speed_controller.error_i = st["shaft_speed_i"]
+    pid = ap.heading_controller.ship_heading_controller
+    pid.error_i, pid.prev_error = st["heading_i"], st["heading_prev"]
+    ap.navigate.e_ct_int = st["e_ct_int"]
+    ap.next_wpt = int(st["next_wpt"])
+
+
+def sim_step(ship, thr, ap, bias=False):
+    """One simulator step as MSRL_Env.obs_step's non-stop path (or test_step if bias)."""
+    rudder = ap.rudder_angle_from_sampled_route(north_position=ship.north, east_position=ship.east,
+                                                heading=ship.yaw_angle)
+    throttle = thr.throttle(speed_set_point=V_DES, measured_speed=ship.forward_speed,
+                            measured_shaft_speed=ship.forward_speed)
+    if bias:
+        throttle *= 0.5
+        throttle = np.clip(throttle, 0.0, 1.1)
+        rudder += np.deg2rad(3)
+        rudder = np.clip(rudder, -ap.heading_controller.max_rudder_angle, ap.heading_controller.max_rudder_angle)
+    ship.store_simulation_data(throttle, rudder, ap.get_cross_track_error(), ap.get_heading_error())
+    ship.update_differentials(engine_throttle=throttle, rudder_angle=rudder)
+    mm = ship.ship_machinery_model
+    out = dict(rudder=float(rudder), throttle=float(throttle), heading_ref=ap.heading_ref,
+               e_ct=ap.navigate.e_ct,
+               rpm=ship.simulation_results["propeller shaft speed [rpm]"][-1],
+               power_me=ship.simulation_results["power me [kw]"][-1],
+               d_north=ship.d_north, d_east=ship.d_east, d_yaw=ship.d_yaw, d_surge=ship.d_forward_speed,
+               d_sway=ship.d_sideways_speed, d_yaw_rate=ship.d_yaw_rate, d_shaft_speed=mm.d_omega,
+               thrust=mm.thrust())
+    ship.integrate_differentials()
+    ship.int.next_time()
+    return out
+
+
+SIM_FIELDS = ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed", "ship_speed_i",
+              "shaft_speed_i", "heading_i", "heading_prev", "e_ct_int", "next_wpt")
+OUT_FIELDS = ("rudder", "throttle", "heading_ref", "e_ct", "rpm", "power_me", "d_north", "d_east", "d_yaw",
+              "d_surge", "d_sway", "d_yaw_rate", "d_shaft_speed", "thrust")
+
+
+def _route_arrays(route):
+    r = np.zeros((CAP, 2))
+    r[:len(route)] = route
+    return r, len(route)
+
+
+def gen_sim_trajectory(ref, name, route, pose, n_steps, bias=False, mode="PTI"):
+    ship, thr, ap = build_ship(ref, route, pose, mode=mode)
+    pre = {k: [] for k in SIM_FIELDS}
+    out = {k: [] for k in OUT_FIELDS}
+    for _ in range(n_steps):
+        snap = ship_snapshot(ship, thr, ap)
+        for k in SIM_FIELDS:
+            pre[k].append(snap[k])
+        o = sim_step(ship, thr, ap, bias)
+        for k in OUT_FIELDS:
+            out[k].append(o[k])
+    snap = ship_snapshot(ship, thr, ap)
+    r, nr = _route_arrays(route)
+    sg, me_cap, el_cap = MODES[mode]
+    data = {"route": r, "n_route": np.int64(nr), "pose": np.asarray(pose, float), "bias": np.int64(bias),
+            "mode": np.asarray([MODE_ID[sg], me_cap, el_cap], float)}
+    for k in SIM_FIELDS:
+        data["pre_" + k] = np.asarray(pre[k] + [snap[k]], dtype=np.float64)
+    for k in OUT_FIELDS:
+        data["out_" + k] = np.asarray(out[k], dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, f"sim_{name}.npz"), **data)
+    return data
+
+
+def gen_sim_teacher_forced(ref, rng, src, n_cases=600):
+    """One-step teacher-forced cases: random pre-states around recorded trajectories plus
+    knife-edge constructions (waypoint acceptance circle, e_ct^2 = r^2, windup limit, throttle < 0)."""
+    route = [[0.0, 0.0], [2500.0, 1500.0], [5000.0, 5200.0], [8500.0, 6500.0], [9500.0, 9500.0]]
+    cases = []
+    T = len(src["pre_north"]) - 1
+    for i in range(n_cases):
+        j = rng.integers(0, T)
+        st = {k: float(src["pre_" + k][j]) for k in SIM_FIELDS}
+        st["next_wpt"] = int(src["pre_next_wpt"][j])
+        kind = i % 8
+        st["north"] += rng.normal(0, 200)
+        st["east"] += rng.normal(0, 200)
+        st["yaw"] += rng.normal(0, 0.5)
+        st["surge"] *= rng.uniform(0.5, 1.5)
+        st["sway"] += rng.normal(0, 0.5)
+        st["yaw_rate"] += rng.normal(0, 0.01)
+        st["shaft_speed"] *= rng.uniform(0.5, 1.5)
+        st["heading_prev"] += rng.normal(0, 0.1)
+        k = st["next_wpt"]
+        if kind == 1:   # on the acceptance circle of waypoint k (+- tiny)
+            ang = rng.uniform(0, 2 * np.pi)
+            rad = 300.0 + rng.choice([-1e-9, 0.0, 1e-9, -1e-3, 1e-3])
+            st["north"] = route[k][0] + rad * math.cos(ang)
+            st["east"] = route[k][1] + rad * math.sin(ang)
+        elif kind == 2:  # |e_ct| around the lookahead distance (clamp branch)
+            a0, a1 = route[k - 1], route[k]
+            al = math.atan2(a1[1] - a0[1], a1[0] - a0[0])
+            off = rng.choice([-1, 1]) * (1000.0 + rng.choice([-1e-6, 0.0, 1e-6, -5.0, 5.0, 300.0]))
+            s = rng.uniform(0.2, 0.8)
+            st["north"] = a0[0] + s * (a1[0] - a0[0]) - off * math.sin(al)
+            st["east"] = a0[1] + s * (a1[1] - a0[1]) + off * math.cos(al)
+        elif kind == 3:  # anti-windup limit
+            st["e_ct_int"] = rng.choice([-1, 1]) * rng.uniform(3999.0, 4000.0)
+        elif kind == 4:  # negative throttle (speed above set point, negative integrators)
+            st["surge"] = rng.uniform(9.0, 14.0)
+            st["ship_speed_i"] = rng.uniform(-50, 10)
+            st["shaft_speed_i"] = rng.uniform(-500, 100)
+        elif kind == 5:  # large heading (unwrapped psi, Q4)
+            st["yaw"] += rng.choice([-1, 1]) * 2 * np.pi * rng.integers(1, 4)
+        elif kind == 6:  # reverse shaft / reverse surge
+            st["shaft_speed"] = -abs(st["shaft_speed"]) * rng.uniform(0.0, 0.5)
+            st["surge"] = -abs(st["surge"]) * rng.uniform(0, 0.5)
+        cases.append(st)
+    pre = {k: [] for k in SIM_FIELDS}
+    post = {k: [] for k in SIM_FIELDS}
+    out = {k: [] for k in OUT_FIELDS}
+    bias = []
+    for i, st in enumerate(cases):
+        ship, thr, ap = build_ship(ref, route, (0, 0, 0, 0, 0, 0))
+        set_ship(ship, thr, ap, st)
+        b = bool(i % 2)
+        snap = ship_snapshot(ship, thr, ap)
+        o = sim_step(ship, thr, ap, bias=b)
+        snap2 = ship_snapshot(ship, thr, ap)
+        for k in SIM_FIELDS:
+            pre[k].append(snap[k])
+            post[k].append(snap2[k])
+        for k in OUT_FIELDS:
+            out[k].append(o[k])
+        bias.append(b)
+    r, nr = _route_arrays(route)
+    data = {"route": r, "n_route": np.int64(nr), "bias": np.asarray(bias, np.int64)}
+    for k in SIM_FIELDS:
+        data["pre_" + k] = np.asarray(pre[k], dtype=np.float64)
+        data["post_" + k] = np.asarray(post[k], dtype=np.float64)
+    for k in OUT_FIELDS:
+        data["out_" + k] = np.asarray(out[k], dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "sim_teacher_forced.npz"), **data)
+
+
+# ---------------------------------------------------------------------------------
+# env-level fixtures (MSRL_env_ex.MultiShipRLEnv under shims)
+# ---------------------------------------------------------------------------------
+ENV_SHIP = ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed", "ship_speed_i",
+            "shaft_speed_i", "heading_i", "heading_prev", "e_ct_int", "last_rpm", "last_e_ct",
+            "last_power_me", "next_wpt", "n_wpt", "ticks", "stop")
+
+
+def make_env(ref, obstacle, env_mod, pose_test, pose_obs, r_test=R_TEST, r_obs=R_OBS, mode="PTI"):
+    ts, tt, ta = build_ship(ref, r_test, pose_test, mode=mode)
+    os_, ot, oa = build_ship(ref, r_obs, pose_obs, mode=mode)
+    A = env_mod.ShipAssets
+    test = A(ship_model=ts, throttle_controller=tt, auto_pilot=ta, desired_forward_speed=V_DES,
+             integrator_term=[], time_list=[], type_tag="test_ship", stop_flag=False)
+    obs = A(ship_model=os_, throttle_controller=ot, auto_pilot=oa, desired_forward_speed=V_DES,
+            integrator_term=[], time_list=[], type_tag="obs_ship", stop_flag=False)
+    env = env_mod.MultiShipRLEnv([test, obs], map=obstacle.PolygonObstacle(MAP), ship_draw=False,
+                                 time_since_last_ship_drawing=30,
+                                 args=SimpleNamespace(sampling_frequency=7, theta=2))
+    return env
+
+
+def env_snapshot(env, iw):
+    snap = {}
+    for t, a in enumerate((env.test, env.obs)):
+        s = ship_snapshot(a.ship_model, a.throttle_controller, a.auto_pilot)
+        s["stop"] = int(bool(a.stop_flag))
+        for k in ENV_SHIP:
+            snap.setdefault(k, [0, 0])[t] = s[k]
+    res = env.obs.ship_model.simulation_results
+    snap["sampling_dist"] = env.sampling_distance_travelled
+    snap["eps_dist"] = env.eps_distance_travelled
+    snap["prev_pre_north"] = res["north position [m]"][-1] if res["north position [m]"] else 0.0
+    snap["prev_pre_east"] = res["east position [m]"][-1] if res["east position [m]"] else 0.0
+    snap["iw_north"], snap["iw_east"] = iw
+    tabs = np.zeros((2, 2, CAP))
+    for t, a in enumerate((env.test, env.obs)):
+        nn, ee = a.auto_pilot.navigate.north, a.auto_pilot.navigate.east
+        tabs[0, t, :len(nn) - 1] = nn[:-1]
+        tabs[1, t, :len(ee) - 1] = ee[:-1]
+    snap["wpt_north"], snap["wpt_east"] = tabs[0], tabs[1]
+    return snap
+
+
+class CaseRecorder:
+    def __init__(self):
+        self.rows = []
+
+    def add(self, **kw):
+        self.rows.append(kw)
+
+    def save(self, path, meta):
+        data = dict(meta)
+        keys = self.rows[0].keys()
+        for k in keys:
+            v = [r[k] for r in self.rows]
+            if k == "status":
+                data[k] = np.asarray(v)
+            else:
+                data[k] = np.asarray(v, dtype=np.float64)
+        np.savez_compressed(path, **data)
+
+
+def run_env_case(ref, obstacle, env_mod, name, n_steps, rng, pose_test=None, pose_obs=None, setup=None,
+                 action_fn=None, resets=(), r_test=R_TEST, r_obs=R_OBS, mode="PTI"):
+    """reset -> init_step -> steps with the synthetic sampler (or action_fn), recording the
+    full pre-state of every step and the step outputs.  Steps listed in `resets` are preceded
+    by reset() + init_step() (episode restart)."""
+    pose_test = pose_test or (R_TEST[0][0], R_TEST[0][1], math.atan2(4000, 300), 0, 0, 0)
+    pose_obs = pose_obs or (R_OBS[0][0], R_OBS[0][1], math.atan2(-100, 6400), 0, 0, 0)
+    env = make_env(ref, obstacle, env_mod, pose_test, pose_obs, r_test, r_obs, mode)
+    rec = CaseRecorder()
+    state0 = env.reset()
+    env.init_step()
+    if setup:
+        setup(env)
+    iw = (0.0, 0.0)
+    t = 1
+    for step in range(n_steps):
+        if step in resets:
+            env.reset()
+            env.init_step()
+            t = 1
+        init = t == 1
+        if action_fn is not None:
+            act, sac = action_fn(env, step, init, iw)
+        else:
+            sample = init or (env.sampling_distance_travelled >= env.AB_segment_length and not env.obs.stop_flag)
+            if sample:
+                a = rng.uniform(-np.pi / 6, np.pi / 6)
+                act = (env.obs.ship_model.north + env.AB_segment_length * np.cos(env.AB_alpha + a),
+                       env.obs.ship_model.east + env.AB_segment_length * np.sin(env.AB_alpha + a))
+            else:
+                act = iw
+            sac = bool(sample)
+        iw = (float(act[0]), float(act[1]))
+        pre = env_snapshot(env, iw)
+        ns, rew, done, status = env.step(iw, sac, init)
+        post = env_snapshot(env, iw)
+        row = {"action_n": iw[0], "action_e": iw[1], "sac_update": float(sac), "init": float(init),
+               "next_state": np.asarray(ns, float), "reward": float(rew), "done": float(done),
+               "status": status}
+        for k, v in pre.items():
+            row["pre_" + k] = np.asarray(v, float)
+        for k, v in post.items():
+            row["post_" + k] = np.asarray(v, float)
+        rec.add(**row)
+        t += 1
+        if done:
+            break
+    routes = np.zeros((2, CAP, 2))
+    routes[0, :len(r_test)] = r_test
+    routes[1, :len(r_obs)] = r_obs
+    sg, me_cap, el_cap = MODES[mode]
+    meta = {"routes": routes, "n_wpt": np.asarray([len(r_test), len(r_obs)], np.int64),
+            "mode": np.asarray([MODE_ID[sg], me_cap, el_cap], float),
+            "pose": np.asarray([pose_test, pose_obs], float), "reset_state": np.asarray(state0),
+            "resets": np.asarray(sorted(resets), np.int64),
+            "ab_len": np.float64(env.AB_segment_length), "ab_alpha": np.float64(env.AB_alpha)}
+    rec.save(os.path.join(HERE, f"env_{name}.npz"), meta)
+    return len(rec.rows)
+
+
+def place(asset, n=None, e=None, yaw=None, surge=None, omega=None, k=None):
+    sm = asset.ship_model
+    if k is not None:
+        asset.auto_pilot.next_wpt = k
+    if n is not None:
+        sm.north = n
+    if e is not None:
+        sm.east = e
+    if yaw is not None:
+        sm.yaw_angle = yaw
+    if surge is not None:
+        sm.forward_speed = surge
+    if omega is not None:
+        sm.ship_machinery_model.omega = omega
+
+
+def gen_env_cases(ref, obstacle, env_mod, seed):
+    rng = np.random.default_rng(seed)
+    n = {}
+    # nominal random-IW episode (runs until done)
+    n["nominal"] = run_env_case(ref, obstacle, env_mod, "nominal", 2500, rng)
+    # obstacle ship arrives -> stop path (time x2, frozen observations), test ship keeps going
+    n["obs_arrival"] = run_env_case(
+        ref, obstacle, env_mod, "obs_arrival", 60, rng,
+        setup=lambda env: place(env.obs, n=8450.0, e=5203.0, surge=8.0),
+        action_fn=lambda env, s, init, iw: ((8500.0, 5200.0), init))
+    # test ship hull corner inside island 4 while on its first leg (terrain, +1000)
+    n["test_terrain"] = run_env_case(
+        ref, obstacle, env_mod, "test_terrain", 200, rng,
+        setup=lambda env: place(env.test, n=1820.0, e=3400.0, yaw=0.5, surge=8.0))
+    # IW sampled inside a polygon (-1000, done) and outside the horizon
+    n["iw_terrain"] = run_env_case(
+        ref, obstacle, env_mod, "iw_terrain", 5, rng,
+        action_fn=lambda env, s, init, iw: ((7000.0, 6500.0), True) if s == 3 else ((3000.0, 5300.0), init))
+    n["iw_horizon"] = run_env_case(
+        ref, obstacle, env_mod, "iw_horizon", 5, rng,
+        action_fn=lambda env, s, init, iw: ((10000.5, 5300.0), True) if s == 2 else ((3000.0, 5300.0), init))
+    # obstacle ship hull in terrain AND IW in terrain at once: -2000 (terrain sets no stop flag)
+    n["obs_terrain_iw"] = run_env_case(
+        ref, obstacle, env_mod, "obs_terrain_iw", 20, rng,
+        setup=lambda env: place(env.obs, n=5540.0, e=5520.0, yaw=0.8, surge=8.0),
+        action_fn=lambda env, s, init, iw: ((6500.0, 6500.0), True))
+    # obstacle ship hull in terrain alone (done without stop flag)
+    n["obs_terrain"] = run_env_case(
+        ref, obstacle, env_mod, "obs_terrain", 20, rng,
+        setup=lambda env: place(env.obs, n=5540.0, e=5520.0, yaw=0.8, surge=8.0),
+        action_fn=lambda env, s, init, iw: ((3000.0, 5300.0), init))
+    # test ship arrival at its endpoint (done, +0)
+    n["test_arrival"] = run_env_case(
+        ref, obstacle, env_mod, "test_arrival", 200, rng,
+        setup=lambda env: place(env.test, n=9150.0, e=9010.0, yaw=0.0, surge=8.0, k=4))
+    # test ship leaves the map (horizon) on a route that points off the south edge
+    n["test_horizon"] = run_env_case(
+        ref, obstacle, env_mod, "test_horizon", 300, rng,
+        r_test=[[600.0, 700.0], [-2000.0, 700.0]], pose_test=(600.0, 700.0, np.pi, 0, 0, 0))
+    # blackout failure: PTO (GEN) and MEC (OFF) machinery modes have main-engine capacity
+    n["blackout_pto"] = run_env_case(ref, obstacle, env_mod, "blackout_pto", 300, rng, mode="PTO")
+    n["mec_nominal"] = run_env_case(ref, obstacle, env_mod, "mec_nominal", 300, rng, mode="MEC")
+    # ship-ship collision (+2000)
+    n["collision"] = run_env_case(
+        ref, obstacle, env_mod, "collision", 200, rng,
+        setup=lambda env: (place(env.test, n=2100.0, e=5300.0, yaw=0.0, surge=8.0),
+                           place(env.obs, n=2200.0, e=5300.0, yaw=np.pi, surge=1.0)))
+    # mechanical failure: shaft speed above 2000 rpm
+    n["mechanical"] = run_env_case(
+        ref, obstacle, env_mod, "mechanical", 5, rng,
+        setup=lambda env: place(env.test, omega=2001.0 * np.pi / 30 + 0.5))
+    # test ship navigation failure (|e_ct| > 1000)
+    n["test_navigation"] = run_env_case(
+        ref, obstacle, env_mod, "test_navigation", 200, rng,
+        setup=lambda env: place(env.test, n=2300.0, e=600.0, yaw=0.0, surge=8.0))
+    # obstacle navigation failure via sampling distance (never resample)
+    n["obs_sampling_nav"] = run_env_case(
+        ref, obstacle, env_mod, "obs_sampling_nav", 2000, rng,
+        action_fn=lambda env, s, init, iw: ((3000.0, 5290.0), init))
+    # reset quirks: persistence of shaft speed and integrators across episodes
+    n["reset_persist"] = run_env_case(ref, obstacle, env_mod, "reset_persist", 400, rng, resets=(150, 151, 300))
+    # many IW insertions (route growth, next_wpt reaching the end, route table stress)
+    n["many_inserts"] = run_env_case(
+        ref, obstacle, env_mod, "many_inserts", 300, rng,
+        action_fn=lambda env, s, init, iw: (((env.obs.ship_model.north + 400.0 * math.cos(0.1 * s),
+                                              env.obs.ship_model.east + 400.0 * math.sin(0.1 * s))), s % 20 == 0))
+    return n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seed", type=int, default=25450)
+    args = ap.parse_args()
+    ref = _import_reference()
+    # C1 / K1: route [[0,0],[10000,10000]], 1000 zero-action steps, no bias
+    gen_sim_trajectory(ref, "c1", [[0.0, 0.0], [10000.0, 10000.0]], (0, 0, np.pi / 4, 0, 0, 0), 1000)
+    # K2: route R_A, 600 steps
+    ra = gen_sim_trajectory(ref, "k2", [[0.0, 0.0], [2500.0, 1500.0], [5000.0, 5200.0], [8500.0, 6500.0],
+                                        [9500.0, 9500.0]], (0, 0, np.pi / 4, 0, 0, 0), 3000)
+    # test-ship variant with the always-on collision bias
+    gen_sim_trajectory(ref, "bias", R_TEST, (R_TEST[0][0], R_TEST[0][1], math.atan2(4000, 300), 0, 0, 0), 1500,
+                       bias=True)
+    gen_sim_trajectory(ref, "pto", R_TEST, (R_TEST[0][0], R_TEST[0][1], math.atan2(4000, 300), 0, 0, 0), 600,
+                       bias=True, mode="PTO")
+    gen_sim_trajectory(ref, "mec", R_OBS, (R_OBS[0][0], R_OBS[0][1], math.atan2(-100, 6400), 0, 0, 0), 300,
+                       mode="MEC")
+    gen_sim_teacher_forced(ref, np.random.default_rng(args.seed), ra)
+    ref2, obstacle, env_mod = install_env_shims()
+    counts = gen_env_cases(ref2, obstacle, env_mod, args.seed)
+    for k, v in counts.items():
+        print(f"env_{k}: {v} steps")
+
+
+if __name__ == "__main__":
+    main()
