@@ -4,7 +4,7 @@
  * This is the drop-in boundary for the one hot path of AndreasKing-Goks/sac-maritime-ast:
  * the two-ship `MultiShipRLEnv` (RLEnv/MSRL_Env.py:37-450, completed by
  * RLEnv/MSRL_env_ex.py:450-980) stepping the ship-in-transit simulator
- * (simulators/ship_in_transit/*.py).  One handle holds N independent two-ship
+ * (the simulators/ship_in_transit package).  One handle holds N independent two-ship
  * environments ("envs"): ship type 0 is the ship under test, type 1 the obstacle
  * ship whose route the AST sampler perturbs with intermediate waypoints (IWs).
  *
@@ -177,6 +177,8 @@ typedef struct sit_params {
 
 /* Fill `p` with the configuration of test_beds/test_policy.py:94-226 (PTI mode). */
 void sit_params_default(sit_params* p);
+/* sizeof(sit_params) as compiled into the library (binding layout check). */
+size_t sit_params_size(void);
 
 /* ---- handle lifecycle ------------------------------------------------------------- */
 typedef struct sit_handle sit_handle;

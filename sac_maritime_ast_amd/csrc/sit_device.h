@@ -1,0 +1,343 @@
+// sit_device.h — device-side building blocks of the ship-in-transit env step (gfx950).
+//
+// Everything here is templated on the real type T (float for the SIT_F32 handle, double for
+// SIT_F64).  The arithmetic follows the reference's operation order where that is free;
+// where a closed form replaces a numpy construct the comment names the reference line:
+//   rotation inverse / mass-matrix inverse      ship_model.py:252-255, 590-603 (closed forms)
+//   wind load, gamma = -atan2(v_rw, u_rw)         ship_model.py:211-231 (trig-free identity)
+//   LOS sin/cos(atan2(dy, dx))                    LOS_guidance.py:110-113 (dy/L, dx/L)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sit {
+
+constexpr int kWave = 64;         // CDNA wavefront
+constexpr int kEnvsPerBlock = 64; // one wave of test ships + one wave of obstacle ships
+constexpr int kMaxPolyVerts = 256;
+constexpr int kMaxPolys = 32;
+
+// --------------------------------------------------------------------------------------
+// math overloads
+// --------------------------------------------------------------------------------------
+__device__ __forceinline__ void xsincos(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ __forceinline__ void xsincos(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __forceinline__ float xatan2(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ double xatan2(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ float xatan(float x) { return atanf(x); }
+__device__ __forceinline__ double xatan(double x) { return atan(x); }
+__device__ __forceinline__ float xsqrt(float x) { return sqrtf(x); }
+__device__ __forceinline__ double xsqrt(double x) { return sqrt(x); }
+__device__ __forceinline__ float xabs(float x) { return fabsf(x); }
+__device__ __forceinline__ double xabs(double x) { return fabs(x); }
+__device__ __forceinline__ float xfma(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ double xfma(double a, double b, double c) { return fma(a, b, c); }
+template <typename T> __device__ __forceinline__ T xmin(T a, T b) { return (b < a) ? b : a; }
+template <typename T> __device__ __forceinline__ T xmax(T a, T b) { return (b > a) ? b : a; }
+// np.clip / PiController.sat: max(low, min(val, hi))
+template <typename T> __device__ __forceinline__ T xclip(T v, T lo, T hi) { return xmax(lo, xmin(v, hi)); }
+
+// --------------------------------------------------------------------------------------
+// constants (derived on the host in double, cast once to T)
+// --------------------------------------------------------------------------------------
+template <typename T>
+struct Consts {
+  T dt;
+  // kinetics (x_g = 0 => diagonal mass matrix)
+  T mass, x_du, y_dv;
+  T inv_m11, inv_m22, inv_m33;
+  T d_u, d_v, d_r;         // linear damping diagonal: m/T_surge, m/T_sway, I_z/T_yaw
+  T ku, kv, kr;            // non-linear damping (signed, Q8)
+  T vc_n, vc_e;            // current in NED
+  T wind_speed, wind_sin, wind_cos;
+  T wk_u, wk_v, wk_n;      // wind load factors (see ship_dynamics)
+  T c_rv, c_rr, rudder_max;
+  // machinery (ship_engine.py:316-395)
+  T avail_prop, avail_me, avail_el, tqcap_me, tqcap_el;
+  T d_me, d_hsg, r_me, r_hsg, kp_prop, jp, thrust_k;
+  T me_cap, hotel, load_el_gen;
+  int32_t sg_mode;
+  int32_t collision_bias;
+  // controllers
+  T kp1, ki1, kp2, ki2, kp_h, kd_h, ki_h;
+  // LOS
+  T los_r, los_r2, los_clamp, los_ki, windup;
+  double ra2;
+  // collision-avoidance bias (MSRL_Env.py:244-251)
+  T bias_scale, bias_max, bias_rudder;
+  // reward / termination (MSRL_env_ex.py)
+  T e_tol, arrival_radius, rpm_max, min_dist2, theta, blackout_kw, rpm_k, half_len;
+  T min_n, max_n, min_e, max_e;
+  T pi6;
+};
+
+// island map: polygon p owns edges [off[p], off[p+1]); edge i goes from vertex i to vertex
+// nxt[i] (ring closed).  Vertex coordinates are (x = east, y = north) as in obstacle.py:128.
+template <typename T>
+struct Map {
+  int32_t n_poly;
+  const int32_t* off;   // [n_poly + 1]
+  const T* vx;          // [n_vert] east
+  const T* vy;          // [n_vert] north
+  const int32_t* nxt;   // [n_vert] index of the next ring vertex
+  const T* inv_len2;    // [n_vert] 1 / |edge|^2 (0 for a degenerate edge)
+  const T* bbox;        // [n_poly][4] min_x, max_x, min_y, max_y
+};
+
+// --------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. SC'11)
+// --------------------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += W0; k1 += W1; }
+    const uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
+    const uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+  }
+}
+
+// 53-bit uniform in [0,1) from Philox(key=seed, ctr=(env_id, event, 0x5A4D, 0))
+__device__ __forceinline__ double sampler_uniform(uint64_t seed, uint64_t env_id, uint32_t event) {
+  uint32_t c[4] = {(uint32_t)env_id, event, 0x5A4Du, 0u};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const double hi = (double)(c[0] >> 5), lo = (double)(c[1] >> 6);
+  return (hi * 67108864.0 + lo) * (1.0 / 9007199254740992.0);
+}
+
+// --------------------------------------------------------------------------------------
+// route access: the body of a ship's route (waypoints 0 .. n_wpt-2) lives in a column of a
+// [cap][stride] table (global or LDS); the final waypoint is held in registers because
+// insertion happens at index -1 (controllers.py:298-303) and never moves it.
+// --------------------------------------------------------------------------------------
+template <typename T>
+struct Route {
+  T* tn;          // column base: entry i at tn[i * stride]
+  T* te;
+  int stride;
+  T end_n, end_e;
+  int nw;         // current number of waypoints
+  __device__ __forceinline__ T n(int i) const { return (i >= nw - 1) ? end_n : tn[i * stride]; }
+  __device__ __forceinline__ T e(int i) const { return (i >= nw - 1) ? end_e : te[i * stride]; }
+};
+
+// --------------------------------------------------------------------------------------
+// one ship
+// --------------------------------------------------------------------------------------
+template <typename T>
+struct Ship {
+  T n, e, psi, u, v, r, w;   // pose, body velocities, shaft speed
+  T i1, i2;                  // ship-speed PI and shaft-speed PI integrals
+  T hi, hp;                  // heading PID integral and previous error
+  T ect_int;                 // LOS cross-track integral
+  T lrpm, lect, lpme;        // last stored observations (stop path)
+  int k;                     // next waypoint index
+  int ticks;                 // simulator time in dt units
+  int stop;                  // ShipAssets.stop_flag
+};
+
+// rudder_angle_from_sampled_route + throttle (controllers.py:306-314, 138-143, 52-62, 81-93,
+// 180-189; LOS_guidance.py:88-121).  Returns rudder, throttle and |e_ct|.
+template <typename T>
+__device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s, const Route<T>& rt,
+                                                 T v_des, T& rudder, T& thr, T& ect_abs) {
+  // next_wpt: acceptance test evaluated in double, without contraction, from the stored
+  // values (bit-identical to the float64 reference for identical inputs)
+  {
+    const double dn = (double)rt.n(s.k) - (double)s.n;
+    const double de = (double)rt.e(s.k) - (double)s.e;
+    const double d2 = __dadd_rn(__dmul_rn(dn, dn), __dmul_rn(de, de));
+    if (d2 <= c.ra2 && rt.nw > s.k + 1) s.k += 1;
+  }
+  const T pn = rt.n(s.k - 1), pe = rt.e(s.k - 1);
+  const T dx = rt.n(s.k) - pn, dy = rt.e(s.k) - pe;
+  const T alpha = xatan2(dy, dx);
+  const T len = xsqrt(dx * dx + dy * dy);
+  T sa = T(0), ca = T(1);
+  if (len > T(0)) { sa = dy / len; ca = dx / len; }
+  T ect = -(s.n - pn) * sa + (s.e - pe) * ca;
+  ect_abs = xabs(ect);
+  if (ect * ect >= c.los_r2) ect = c.los_clamp;           // sign lost (Q5)
+  const T delta = xsqrt(c.los_r2 - ect * ect);
+  const T q = ect / delta;
+  if (xabs(s.ect_int + q) <= c.windup) s.ect_int += q;
+  const T chi = xatan(-q - s.ect_int * c.los_ki);
+  const T psi_ref = alpha + chi;
+  // heading PID, error not wrapped (Q4)
+  const T err = psi_ref - s.psi;
+  const T derr = (err - s.hp) / c.dt;
+  s.hi = s.hi + err * c.dt;
+  s.hp = err;
+  const T out = err * c.kp_h + derr * c.kd_h + s.hi * c.ki_h;
+  rudder = xclip(-out, -c.rudder_max, c.rudder_max);
+  // cascaded PI, shaft PI measures the ship speed (Q2), no saturation (Q3)
+  const T e1 = v_des - s.u;
+  s.i1 = s.i1 + e1 * c.dt;
+  const T wdes = e1 * c.kp1 + s.i1 * c.ki1;
+  const T e2 = wdes - s.u;
+  s.i2 = s.i2 + e2 * c.dt;
+  thr = e2 * c.kp2 + s.i2 * c.ki2;
+}
+
+// distribute_load(...).load_on_main_engine / 1000 (ship_engine.py:46-76)
+template <typename T>
+__device__ __forceinline__ T power_me_kw(const Consts<T>& c, T thr) {
+  const T total = thr * c.avail_prop;
+  T load_me;
+  if (c.sg_mode == 0) load_me = xmin(total, c.me_cap);                  // MOTOR
+  else if (c.sg_mode == 1) load_me = total + c.hotel - c.load_el_gen;    // GEN
+  else load_me = total;                                                 // OFF
+  return load_me / T(1000);
+}
+
+// update_differentials + integrate_differentials (ship_model.py:624-643, ship_engine.py:355-395)
+template <typename T>
+__device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T thr, T rudder) {
+  T sp, cp;
+  xsincos(s.psi, &sp, &cp);
+  const T u = s.u, v = s.v, r = s.r, w = s.w;
+  // kinematics: eta_dot = R(psi) nu
+  const T d_n = cp * u - sp * v;
+  const T d_e = sp * u + cp * v;
+  // shaft equation with pre-step omega
+  const T tq_me = xmin(thr * c.avail_me / (w + T(0.1)), c.tqcap_me);
+  const T tq_hsg = xmin(thr * c.avail_el / (w + T(0.1)), c.tqcap_el);
+  const T d_w = ((tq_me - c.d_me * w) / c.r_me + (tq_hsg - c.d_hsg * w) / c.r_hsg - c.kp_prop * (w * w)) / c.jp;
+  const T thrust = c.thrust_k * w * xabs(w);
+  // current in body frame: R(psi)^T v_c
+  const T vc_u = cp * c.vc_n + sp * c.vc_e;
+  const T vc_v = -sp * c.vc_n + cp * c.vc_e;
+  const T ur = u - vc_u, vr = v - vc_v;
+  // rudder forces (ship_model.py:608-622)
+  const T f_rv = -c.c_rv * rudder * ur;
+  const T f_rr = -c.c_rr * rudder * ur;
+  // wind (ship_model.py:211-231): with gamma = -atan2(v_rw, u_rw), cos g = u_rw/|w|,
+  // sin g = -v_rw/|w|, so tau = (-0.5 rho cx Af |w| u_rw, -0.5 rho cy Al |w| v_rw,
+  // -rho cn Al L u_rw v_rw)
+  const T uw = c.wind_speed * (c.wind_cos * cp + c.wind_sin * sp);   // cos(beta - psi)
+  const T vw = c.wind_speed * (c.wind_sin * cp - c.wind_cos * sp);   // sin(beta - psi)
+  const T urw = uw - u, vrw = vw - v;
+  const T wmag = xsqrt(urw * urw + vrw * vrw);
+  const T tau_u = c.wk_u * wmag * urw;
+  const T tau_v = c.wk_v * wmag * vrw;
+  const T tau_n = c.wk_n * urw * vrw;
+  // -C_RB nu - C_A(nu_r) nu_r - (D + D_n) nu_r + tau  (ship_model.py:596-603)
+  const T mv = c.mass * v, mu = c.mass * u;
+  const T yv = c.y_dv * vr, xu = c.x_du * ur;
+  const T f0 = mv * r - yv * r - (c.d_u + c.ku * u) * ur + tau_u + thrust;
+  const T f1 = -mu * r + xu * r - (c.d_v + c.kv * v) * vr + tau_v + f_rv;
+  const T f2 = -(mv * u - mu * v) - (-yv * ur + xu * vr) - (c.d_r + c.kr * r) * r + tau_n + f_rr;
+  // Euler (utils.py:50-53)
+  s.n = s.n + d_n * c.dt;
+  s.e = s.e + d_e * c.dt;
+  s.psi = s.psi + r * c.dt;
+  s.u = u + (c.inv_m11 * f0) * c.dt;
+  s.v = v + (c.inv_m22 * f1) * c.dt;
+  s.r = r + (c.inv_m33 * f2) * c.dt;
+  s.w = w + d_w * c.dt;
+}
+
+// --------------------------------------------------------------------------------------
+// polygon predicates (obstacle.py:126-141 -> GEOS)
+// --------------------------------------------------------------------------------------
+// exact sign of a*b - c*d (TwoProduct via fma, Shewchuk grow-expansion)
+template <typename T>
+__device__ __forceinline__ int exact_sign_diff(T a, T b, T c, T d) {
+  const T p1 = a * b, e1 = xfma(a, b, -p1);
+  const T p2 = c * d, e2 = xfma(c, d, -p2);
+  auto two_sum = [](T x, T y, T& err) { const T s = x + y; const T bb = s - x; err = (x - (s - bb)) + (y - bb); return s; };
+  T h0, h1, g0, g1, g2;
+  T q = two_sum(-e2, e1, h0);
+  q = two_sum(q, p1, h1);
+  const T h2 = q;
+  T q2 = two_sum(-p2, h0, g0);
+  q2 = two_sum(q2, h1, g1);
+  q2 = two_sum(q2, h2, g2);
+  const T comps[4] = {q2, g2, g1, g0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (comps[i] > T(0)) return 1;
+    if (comps[i] < T(0)) return -1;
+  }
+  return 0;
+}
+
+// GEOS CGAlgorithmsDD::orientationIndex(p1, p2, q): orientationIndexFilter, exact fallback
+template <typename T>
+__device__ __forceinline__ int orientation(T p1x, T p1y, T p2x, T p2y, T qx, T qy) {
+#pragma clang fp contract(off)
+  const T ax = p1x - qx, by = p2y - qy, ay = p1y - qy, bx = p2x - qx;
+  const T dl = ax * by;
+  const T dr = ay * bx;
+  const T det = dl - dr;
+  const bool same = (dl > T(0) && dr > T(0)) || (dl < T(0) && dr < T(0));
+  if (!same || xabs(det) >= T(1e-15) * (xabs(dl) + xabs(dr))) return (det > T(0)) - (det < T(0));
+  return exact_sign_diff(ax, by, ay, bx);
+}
+
+// Polygon.contains(Point(e, n)) for any polygon: GEOS RayCrossingCounter (strict interior)
+template <typename T>
+__device__ bool point_in_polys(const Map<T>& m, T n, T e) {
+  const T qx = e, qy = n;
+  bool inside = false;
+  for (int p = 0; p < m.n_poly; ++p) {
+    const T* bb = m.bbox + 4 * p;
+    if (qx < bb[0] || qx > bb[1] || qy < bb[2] || qy > bb[3]) continue;
+    int cross = 0;
+    bool onb = false;
+    for (int i = m.off[p]; i < m.off[p + 1]; ++i) {
+      const T p1x = m.vx[i], p1y = m.vy[i];
+      const int j = m.nxt[i];
+      const T p2x = m.vx[j], p2y = m.vy[j];
+      if (p1x < qx && p2x < qx) continue;
+      if (qx == p2x && qy == p2y) { onb = true; break; }
+      if (p1y == qy && p2y == qy) {
+        if (xmin(p1x, p2x) <= qx && qx <= xmax(p1x, p2x)) { onb = true; break; }
+        continue;
+      }
+      if ((p1y > qy && p2y <= qy) || (p2y > qy && p1y <= qy)) {
+        int o = orientation(p1x, p1y, p2x, p2y, qx, qy);
+        if (o == 0) { onb = true; break; }
+        if (p2y < p1y) o = -o;
+        if (o > 0) ++cross;
+      }
+    }
+    inside |= (!onb && (cross & 1));
+  }
+  return inside;
+}
+
+// min over polygons of exterior.distance(Point(e, n)) (GEOS Distance::pointToSegment),
+// evaluated on squared distances with one final sqrt.
+template <typename T>
+__device__ T distance_to_polys(const Map<T>& m, T n, T e) {
+  const T px = e, py = n;
+  T best = T(3.0e38);
+  const int nv = m.off[m.n_poly];
+  for (int i = 0; i < nv; ++i) {
+    const T ax = m.vx[i], ay = m.vy[i];
+    const int j = m.nxt[i];
+    const T bx = m.vx[j], by = m.vy[j];
+    const T ex = bx - ax, ey = by - ay;
+    const T qx = px - ax, qy = py - ay;
+    const T t = qx * ex + qy * ey;
+    const T il2 = m.inv_len2[i];
+    T d2;
+    if (il2 == T(0) || t <= T(0)) {
+      d2 = qx * qx + qy * qy;
+    } else if (t * il2 >= T(1)) {
+      const T rx = px - bx, ry = py - by;
+      d2 = rx * rx + ry * ry;
+    } else {
+      const T cr = qy * ex - qx * ey;
+      d2 = cr * cr * il2;
+    }
+    best = xmin(best, d2);
+  }
+  return xsqrt(best);
+}
+
+}  // namespace sit

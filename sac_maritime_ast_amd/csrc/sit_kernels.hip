@@ -1,0 +1,1118 @@
+// sit_kernels.hip — MI355X (gfx950) kernels and C ABI of the ship-in-transit env step.
+//
+// Layout in HBM (struct of arrays, one device blob, every field 256-B aligned):
+//   ship fields  [2][n_env]   index = type * n_env + env (type 0 = ship under test, 1 = obstacle)
+//   env fields   [n_env]
+//   route tables [2][cap][n_env]  (north and east; waypoint i of env e's ship t at
+//                                  (t * cap + i) * n_env + e, so a wave reads one waypoint
+//                                  index of 64 envs as one coalesced line set)
+// Thread mapping of the step kernel: a 128-thread block owns 64 envs; wave 0 steps their test
+// ships, wave 1 their obstacle ships (different control flow per wave, none inside a wave).
+// The env-level reward needs both ships: each wave evaluates its own ship's termination
+// predicates, the two waves exchange through LDS (double-buffered slots, one barrier per step)
+// and the test-ship wave assembles reward/done/status in the reference's summation order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "sit.h"
+#include "sit_device.h"
+
+using namespace sit;
+
+// ---------------------------------------------------------------------------------------
+// state blob description
+// ---------------------------------------------------------------------------------------
+namespace {
+
+enum Extent { kShip = 0, kEnv = 1, kTable = 2 };
+struct FieldSpec {
+  const char* name;
+  int dtype;
+  int extent;
+};
+
+constexpr int kShipReal = 15;
+constexpr int kEnvReal = 6;
+const FieldSpec kFields[] = {
+    {"north", SIT_DT_REAL, kShip},        {"east", SIT_DT_REAL, kShip},
+    {"yaw", SIT_DT_REAL, kShip},          {"surge", SIT_DT_REAL, kShip},
+    {"sway", SIT_DT_REAL, kShip},         {"yaw_rate", SIT_DT_REAL, kShip},
+    {"shaft_speed", SIT_DT_REAL, kShip},  {"ship_speed_i", SIT_DT_REAL, kShip},
+    {"shaft_speed_i", SIT_DT_REAL, kShip}, {"heading_i", SIT_DT_REAL, kShip},
+    {"heading_prev", SIT_DT_REAL, kShip}, {"e_ct_int", SIT_DT_REAL, kShip},
+    {"last_rpm", SIT_DT_REAL, kShip},     {"last_e_ct", SIT_DT_REAL, kShip},
+    {"last_power_me", SIT_DT_REAL, kShip},
+    {"next_wpt", SIT_DT_I32, kShip},      {"n_wpt", SIT_DT_I32, kShip},
+    {"ticks", SIT_DT_I32, kShip},         {"stop", SIT_DT_I32, kShip},
+    {"sampling_dist", SIT_DT_REAL, kEnv}, {"eps_dist", SIT_DT_REAL, kEnv},
+    {"prev_pre_north", SIT_DT_REAL, kEnv}, {"prev_pre_east", SIT_DT_REAL, kEnv},
+    {"iw_north", SIT_DT_REAL, kEnv},      {"iw_east", SIT_DT_REAL, kEnv},
+    {"ep_step", SIT_DT_I32, kEnv},        {"event", SIT_DT_U32, kEnv},
+    {"episodes", SIT_DT_U32, kEnv},
+    {"wpt_north", SIT_DT_REAL, kTable},   {"wpt_east", SIT_DT_REAL, kTable},
+};
+constexpr int kNumFields = (int)(sizeof(kFields) / sizeof(kFields[0]));
+enum FieldId {
+  F_NORTH = 0, F_LAST_PME = 14, F_K = 15, F_NW, F_TICKS, F_STOP,
+  F_SAMP = 19, F_IW_E = 24, F_EP = 25, F_EVENT, F_EPISODES, F_WN, F_WE
+};
+
+// per-env scenario (constant after sit_load_*), device side
+template <typename T>
+struct Scen {
+  const T* init;          // [2][SIT_INIT_NF][n_env]
+  const T* end_n;         // [2][n_env]
+  const T* end_e;
+  const int32_t* nw0;     // [2][n_env]
+  const double* ab_len;   // [n_env]
+  const double* ab_alpha; // [n_env]
+  const T* initial_state; // [n_env][10]
+};
+
+template <typename T>
+struct State {
+  T* ship[kShipReal];     // [2 * n_env]
+  int32_t* k;
+  int32_t* nw;
+  int32_t* ticks;
+  int32_t* stop;
+  T* env[kEnvReal];       // sampling_dist, eps_dist, prev_pre_n, prev_pre_e, iw_n, iw_e
+  int32_t* ep_step;
+  uint32_t* event;
+  uint32_t* episodes;
+  T* wn;                  // [2][cap][n_env]
+  T* we;
+};
+
+template <typename T>
+struct StepIO {
+  int32_t n_steps;
+  int32_t auto_reset;
+  uint64_t seed;
+  int64_t env_id_offset;
+  const T* action_ne;
+  const uint8_t* sac_update;
+  const uint8_t* init;
+  T* next_state;
+  T* reward;
+  uint8_t* done;
+  uint32_t* status;
+  T* action_out;
+  int32_t* done_count;
+};
+
+template <typename T>
+struct KArgs {
+  Consts<T> c;
+  Map<T> map;
+  State<T> st;
+  Scen<T> sc;
+  StepIO<T> io;
+  int32_t n_env;
+  int32_t cap;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// device helpers on the SoA state
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void load_ship(const State<T>& st, int sid, Ship<T>& s) {
+  s.n = st.ship[0][sid]; s.e = st.ship[1][sid]; s.psi = st.ship[2][sid];
+  s.u = st.ship[3][sid]; s.v = st.ship[4][sid]; s.r = st.ship[5][sid]; s.w = st.ship[6][sid];
+  s.i1 = st.ship[7][sid]; s.i2 = st.ship[8][sid]; s.hi = st.ship[9][sid]; s.hp = st.ship[10][sid];
+  s.ect_int = st.ship[11][sid]; s.lrpm = st.ship[12][sid]; s.lect = st.ship[13][sid];
+  s.lpme = st.ship[14][sid];
+  s.k = st.k[sid]; s.ticks = st.ticks[sid]; s.stop = st.stop[sid];
+}
+
+template <typename T>
+__device__ __forceinline__ void store_ship(const State<T>& st, int sid, const Ship<T>& s) {
+  st.ship[0][sid] = s.n; st.ship[1][sid] = s.e; st.ship[2][sid] = s.psi;
+  st.ship[3][sid] = s.u; st.ship[4][sid] = s.v; st.ship[5][sid] = s.r; st.ship[6][sid] = s.w;
+  st.ship[7][sid] = s.i1; st.ship[8][sid] = s.i2; st.ship[9][sid] = s.hi; st.ship[10][sid] = s.hp;
+  st.ship[11][sid] = s.ect_int; st.ship[12][sid] = s.lrpm; st.ship[13][sid] = s.lect;
+  st.ship[14][sid] = s.lpme;
+  st.k[sid] = s.k; st.ticks[sid] = s.ticks; st.stop[sid] = s.stop;
+}
+
+template <typename T>
+__device__ __forceinline__ T init_val(const Scen<T>& sc, int type, int f, int env, int n_env) {
+  return sc.init[(type * SIT_INIT_NF + f) * n_env + env];
+}
+
+// MultiShipRLEnv.reset for one ship (MSRL_Env.py:147-188): pose/velocities/time/route/LOS
+// reset; shaft speed and every PI/PID integrator persist (Q6).
+template <typename T>
+__device__ __forceinline__ void reset_ship(const Scen<T>& sc, int type, int env, int n_env, Ship<T>& s,
+                                           int& nw) {
+  s.n = init_val(sc, type, SIT_INIT_NORTH, env, n_env);
+  s.e = init_val(sc, type, SIT_INIT_EAST, env, n_env);
+  s.psi = init_val(sc, type, SIT_INIT_YAW, env, n_env);
+  s.u = init_val(sc, type, SIT_INIT_SURGE, env, n_env);
+  s.v = init_val(sc, type, SIT_INIT_SWAY, env, n_env);
+  s.r = init_val(sc, type, SIT_INIT_YAW_RATE, env, n_env);
+  s.ect_int = T(0);
+  s.k = 1;
+  s.ticks = 0;
+  s.stop = 0;
+  nw = sc.nw0[type * n_env + env];
+}
+
+// one guidance/control/update/integrate cycle without store, time or bias (MSRL_Env.py:190-217)
+template <typename T>
+__device__ __forceinline__ void init_step_ship(const Consts<T>& c, Ship<T>& s, const Route<T>& rt, T v_des) {
+  T rudder, thr, ect;
+  guidance_control(c, s, rt, v_des, rudder, thr, ect);
+  ship_dynamics(c, s, thr, rudder);
+}
+
+// map bounds check of is_pos_outside_horizon / is_route_outside_horizon (MSRL_env_ex.py:460-542)
+template <typename T>
+__device__ __forceinline__ bool outside(const Consts<T>& c, T n, T e, T margin) {
+  return n < c.min_n + margin || n > c.max_n - margin || e < c.min_e + margin || e > c.max_e - margin;
+}
+
+// is_pos_inside_obstacles: 4 corners of a +-l/2 square (MSRL_env_ex.py:490-515)
+template <typename T>
+__device__ __forceinline__ bool hull_in_terrain(const Consts<T>& c, const Map<T>& m, T n, T e) {
+  const T h = c.half_len;
+  return point_in_polys(m, n - h, e - h) | point_in_polys(m, n - h, e + h) |
+         point_in_polys(m, n + h, e - h) | point_in_polys(m, n + h, e + h);
+}
+
+constexpr uint32_t kStopBit = 1u << 30;   // exchange-only: stop flag after this ship's checks
+constexpr uint32_t kDoneBit = 1u << 29;   // exchange-only: this ship's done
+
+template <typename T>
+struct Xchg {
+  T n[2][kWave];
+  T e[2][kWave];
+  T r_nto[kWave];
+  T r_o[kWave];
+  uint32_t bits[2][kWave];
+};
+
+// ---------------------------------------------------------------------------------------
+// the env step kernel: K steps of MultiShipRLEnv.step (+ optional auto-reset)
+//   SYNTH : actions from the synthetic AST sampler (else explicit arrays)
+//   STAGE : route tables staged in LDS for the K steps (else read in place from HBM)
+// ---------------------------------------------------------------------------------------
+template <typename T, bool SYNTH, bool STAGE>
+__global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ Xchg<T> xs[2];
+  const Consts<T>& c = a.c;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int type = threadIdx.x >> 6;             // wave-uniform
+  const int n_env = a.n_env;
+  const int env = blockIdx.x * kEnvsPerBlock + lane;
+  const bool act = env < n_env;
+  const int sid = type * n_env + env;
+
+  Ship<T> s{};
+  Route<T> rt{};
+  T v_des = T(0);
+  T samp = T(0), eps = T(0), ppn = T(0), ppe = T(0), iwn = T(0), iwe = T(0);
+  int ep_step = 0;
+  uint32_t event = 0, episodes = 0;
+  double ab_len = 0.0, ab_alpha = 0.0;
+  if (act) {
+    load_ship(a.st, sid, s);
+    rt.nw = a.st.nw[sid];
+    rt.end_n = a.sc.end_n[sid];
+    rt.end_e = a.sc.end_e[sid];
+    v_des = init_val(a.sc, type, SIT_INIT_DESIRED_SPEED, env, n_env);
+    T* gn = a.st.wn + (size_t)type * a.cap * n_env + env;
+    T* ge = a.st.we + (size_t)type * a.cap * n_env + env;
+    if (STAGE) {
+      T* ln = reinterpret_cast<T*>(smem) + (size_t)type * a.cap * kWave + lane;
+      T* le = ln + (size_t)2 * a.cap * kWave;
+      for (int i = 0; i < rt.nw - 1; ++i) {
+        ln[i * kWave] = gn[(size_t)i * n_env];
+        le[i * kWave] = ge[(size_t)i * n_env];
+      }
+      rt.tn = ln; rt.te = le; rt.stride = kWave;
+    } else {
+      rt.tn = gn; rt.te = ge; rt.stride = n_env;
+    }
+    if (type == 1) {
+      samp = a.st.env[0][env]; eps = a.st.env[1][env];
+      ppn = a.st.env[2][env]; ppe = a.st.env[3][env];
+      iwn = a.st.env[4][env]; iwe = a.st.env[5][env];
+      ep_step = a.st.ep_step[env];
+      event = a.st.event[env];
+      episodes = a.st.episodes[env];
+      ab_len = a.sc.ab_len[env];
+      ab_alpha = a.sc.ab_alpha[env];
+    }
+  }
+  const T maxn = c.max_n;
+
+  for (int step = 0; step < a.io.n_steps; ++step) {
+    const size_t row = (size_t)step * n_env + env;
+    Xchg<T>& x = xs[step & 1];
+    // ---------------- own ship ----------------
+    T o_rpm = T(0), o_ect = T(0), o_pme = T(0);
+    T r_nt = T(0), r_term = T(0);
+    uint32_t bits = 0;
+    bool sac = false, init_f = false;
+    double ang = NAN;
+    if (act) {
+      if (type == 1) {
+        // converted_action / SAC_update / init of this step
+        if (SYNTH) {
+          init_f = (ep_step == 0);
+          sac = init_f || ((double)samp >= ab_len && !s.stop);
+          if (sac) {
+            const double u01 = sampler_uniform(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
+            ang = (u01 * 2.0 - 1.0) * (M_PI / 6.0);
+            iwn = (T)((double)s.n + ab_len * cos(ab_alpha + ang));
+            iwe = (T)((double)s.e + ab_len * sin(ab_alpha + ang));
+            ++event;
+          }
+        } else {
+          init_f = a.io.init[row] != 0;
+          sac = a.io.sac_update[row] != 0;
+          iwn = a.io.action_ne[2 * row];
+          iwe = a.io.action_ne[2 * row + 1];
+        }
+        // obs_step (MSRL_Env.py:287-402)
+        if (s.stop) {
+          s.ticks += 2;                  // stop path: next_time() twice, no integration (Q10)
+          o_rpm = s.lrpm; o_ect = s.lect; o_pme = s.lpme;
+        } else {
+          if (sac) {                     // update_route: insert at index -1 (Q16)
+            if (rt.nw < a.cap) {
+              const int i = rt.nw - 1;
+              rt.tn[i * rt.stride] = iwn;
+              rt.te[i * rt.stride] = iwe;
+              rt.nw += 1;
+            } else {
+              bits |= SIT_ST_ROUTE_OVERFLOW;
+            }
+            samp = T(0);
+          }
+          const T pre_n = s.n, pre_e = s.e;
+          T rudder, thr;
+          guidance_control(c, s, rt, v_des, rudder, thr, o_ect);
+          o_rpm = s.w * T(30) / T(M_PI);
+          o_pme = power_me_kw(c, thr);
+          s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
+          ship_dynamics(c, s, thr, rudder);
+          if (!init_f) {                 // distance between the last two stored positions
+            const T dn = pre_n - ppn, de = pre_e - ppe;
+            const T d = xsqrt(dn * dn + de * de);
+            eps = eps + d;
+            samp = samp + d;
+          }
+          ppn = pre_n; ppe = pre_e;
+          s.ticks += 1;
+        }
+      } else {
+        // test_step (MSRL_Env.py:219-285)
+        T rudder, thr;
+        guidance_control(c, s, rt, v_des, rudder, thr, o_ect);
+        if (c.collision_bias) {          // is_collision_imminent() on all-zero states (Q1)
+          thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
+          rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
+        }
+        o_rpm = s.w * T(30) / T(M_PI);
+        o_pme = power_me_kw(c, thr);
+        s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
+        ship_dynamics(c, s, thr, rudder);
+        s.ticks += 1;
+      }
+
+      // ---------------- own termination predicates (MSRL_env_ex.py:628-881) ----------------
+      const T dobst = distance_to_polys(a.map, s.n, s.e);
+      const T dn_end = s.n - rt.end_n, de_end = s.e - rt.end_e;
+      const bool arrive = xsqrt(dn_end * dn_end + de_end * de_end) <= c.arrival_radius;
+      const bool horizon = outside(c, s.n, s.e, c.half_len);
+      const bool terrain = hull_in_terrain(c, a.map, s.n, s.e);
+      int stop = s.stop;
+      bool done = false;
+      if (type == 0) {
+        r_nt = xabs(o_ect) / c.e_tol + (T(1) - dobst / maxn) / T(100);
+        const bool pred[6] = {arrive, horizon, terrain, xabs(o_rpm) > c.rpm_max, xabs(o_ect) > c.e_tol,
+                              o_pme > c.blackout_kw};
+        const T rew[6] = {T(0), T(0), T(1000), T(1000), T(1000), T(1000)};
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          if (pred[i]) {
+            if (!stop) r_term = r_term + rew[i];
+            stop = 1;
+            done = true;
+            bits |= 1u << i;
+          }
+        }
+        if (done) bits |= SIT_ST_TEST_DONE;
+      } else {
+        if (!stop)
+          r_nt = T(0.1) + (-(xabs(o_ect) / c.e_tol)) / T(100) + (-(T(1) - dobst / maxn)) / T(100);
+        if (arrive) { stop = 1; bits |= SIT_ST_OBS_ENDPOINT; }
+        if (horizon) { stop = 1; done = true; bits |= SIT_ST_OBS_HORIZON; }
+        if (terrain) {                   // done without stop flag (Q12)
+          if (!stop) r_term = r_term - T(1000);
+          done = true;
+          bits |= SIT_ST_OBS_TERRAIN;
+        }
+        if (outside(c, iwn, iwe, T(0)) || point_in_polys(a.map, iwn, iwe)) {   // Q11
+          if (!stop) r_term = r_term - T(1000);
+          stop = 1; done = true;
+          bits |= SIT_ST_OBS_IW_TERMINAL;
+        }
+        if (xabs(o_ect) > c.e_tol || (double)samp > ab_len * (double)c.theta) {
+          if (!stop) r_term = r_term - T(1000);
+          stop = 1; done = true;
+          bits |= SIT_ST_OBS_NAVIGATION;
+        }
+        if (done) bits |= SIT_ST_OBS_DONE;
+      }
+      s.stop = stop;
+      x.n[type][lane] = s.n;
+      x.e[type][lane] = s.e;
+      x.bits[type][lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u);
+      if (type == 1) { x.r_nto[lane] = r_nt; x.r_o[lane] = r_term; }
+    }
+    __syncthreads();
+    // ---------------- env level: shared reward, outputs ----------------
+    bool env_done = false;
+    if (act) {
+      const T dn = x.n[0][lane] - x.n[1][lane], de = x.e[0][lane] - x.e[1][lane];
+      const bool coll = dn * dn + de * de < c.min_dist2;
+      const uint32_t bt = x.bits[0][lane], bo = x.bits[1][lane];
+      env_done = ((bt | bo) & kDoneBit) || coll;
+      if (coll) s.stop = 1;
+      if (type == 0) {
+        const T r_snt = (bo & kStopBit) ? T(0) : (T(1) - xsqrt(dn * dn + de * de) / maxn) / T(1000);
+        const T rs = coll ? T(2000) : T(0);
+        const T reward = r_nt + r_term + x.r_nto[lane] + x.r_o[lane] + r_snt + rs;
+        const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
+        if (a.io.reward) a.io.reward[row] = reward;
+        if (a.io.done) a.io.done[row] = env_done ? 1 : 0;
+        if (a.io.status) a.io.status[row] = status;
+        if (a.io.next_state) {
+          T* ns = a.io.next_state + row * SIT_OBS_DIM;
+          ns[0] = s.n; ns[1] = s.e; ns[2] = s.psi; ns[3] = o_rpm; ns[4] = o_ect; ns[5] = o_pme;
+        }
+      } else {
+        if (a.io.next_state) {
+          T* ns = a.io.next_state + row * SIT_OBS_DIM;
+          ns[6] = s.n; ns[7] = s.e; ns[8] = s.psi; ns[9] = o_ect;
+        }
+        if (a.io.action_out) {
+          T* ao = a.io.action_out + row * 4;
+          ao[0] = iwn; ao[1] = iwe; ao[2] = (T)ang; ao[3] = sac ? T(1) : T(0);
+        }
+      }
+    }
+    // episode-done count: one ballot + popcount per wave, one atomic per wave
+    if (type == 0 && a.io.done_count) {
+      const unsigned long long m = __ballot(env_done);
+      if (lane == 0 && m) atomicAdd(a.io.done_count + step, (int)__popcll(m));
+    }
+    // ---------------- auto reset: reset() + init_step() (test_beds/main_ast.py:314-329) ----------------
+    if (act) {
+      if (type == 1) ep_step += 1;
+      if (a.io.auto_reset && env_done) {
+        reset_ship(a.sc, type, env, n_env, s, rt.nw);
+        if (type == 1) { samp = T(0); eps = T(0); ep_step = 0; ++episodes; }
+        init_step_ship(c, s, rt, v_des);
+      }
+    }
+  }
+
+  // ---------------- write back ----------------
+  if (act) {
+    store_ship(a.st, sid, s);
+    a.st.nw[sid] = rt.nw;
+    if (STAGE) {
+      T* gn = a.st.wn + (size_t)type * a.cap * n_env + env;
+      T* ge = a.st.we + (size_t)type * a.cap * n_env + env;
+      for (int i = 0; i < rt.nw - 1; ++i) {
+        gn[(size_t)i * n_env] = rt.tn[i * kWave];
+        ge[(size_t)i * n_env] = rt.te[i * kWave];
+      }
+    }
+    if (type == 1) {
+      a.st.env[0][env] = samp; a.st.env[1][env] = eps;
+      a.st.env[2][env] = ppn; a.st.env[3][env] = ppe;
+      a.st.env[4][env] = iwn; a.st.env[5][env] = iwe;
+      a.st.ep_step[env] = ep_step;
+      a.st.event[env] = event;
+      a.st.episodes[env] = episodes;
+    }
+  }
+}
+
+// MultiShipRLEnv.init_step for masked envs (one thread per ship)
+template <typename T>
+__global__ __launch_bounds__(256) void k_init_step(const KArgs<T> a, const uint8_t* mask) {
+  const int sid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_env = a.n_env;
+  if (sid >= 2 * n_env) return;
+  const int type = sid / n_env, env = sid - type * n_env;
+  if (mask && !mask[env]) return;
+  Ship<T> s;
+  load_ship(a.st, sid, s);
+  Route<T> rt;
+  rt.nw = a.st.nw[sid];
+  rt.end_n = a.sc.end_n[sid];
+  rt.end_e = a.sc.end_e[sid];
+  rt.tn = a.st.wn + (size_t)type * a.cap * n_env + env;
+  rt.te = a.st.we + (size_t)type * a.cap * n_env + env;
+  rt.stride = n_env;
+  init_step_ship(a.c, s, rt, init_val(a.sc, type, SIT_INIT_DESIRED_SPEED, env, n_env));
+  store_ship(a.st, sid, s);
+}
+
+// MultiShipRLEnv.reset for masked envs (one thread per env)
+template <typename T>
+__global__ __launch_bounds__(256) void k_reset(const KArgs<T> a, const uint8_t* mask, T* initial_state) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_env = a.n_env;
+  if (env >= n_env) return;
+  if (!mask || mask[env]) {
+    for (int type = 0; type < 2; ++type) {
+      const int sid = type * n_env + env;
+      Ship<T> s;
+      load_ship(a.st, sid, s);
+      int nw;
+      reset_ship(a.sc, type, env, n_env, s, nw);
+      store_ship(a.st, sid, s);
+      a.st.nw[sid] = nw;
+    }
+    a.st.env[0][env] = T(0);
+    a.st.env[1][env] = T(0);
+    a.st.ep_step[env] = 0;
+    if (initial_state)
+      for (int j = 0; j < SIT_OBS_DIM; ++j) initial_state[(size_t)env * SIT_OBS_DIM + j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
+  }
+}
+
+// construction-time state (one thread per env)
+template <typename T>
+__global__ __launch_bounds__(256) void k_restart(const KArgs<T> a) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_env = a.n_env;
+  if (env >= n_env) return;
+  for (int type = 0; type < 2; ++type) {
+    const int sid = type * n_env + env;
+    Ship<T> s{};
+    int nw;
+    reset_ship(a.sc, type, env, n_env, s, nw);
+    s.w = init_val(a.sc, type, SIT_INIT_SHAFT_SPEED, env, n_env);
+    s.i1 = init_val(a.sc, type, SIT_INIT_SHIP_SPEED_I, env, n_env);
+    s.i2 = init_val(a.sc, type, SIT_INIT_SHAFT_SPEED_I, env, n_env);
+    s.hi = T(0); s.hp = T(0); s.lrpm = T(0); s.lect = T(0); s.lpme = T(0);
+    store_ship(a.st, sid, s);
+    a.st.nw[sid] = nw;
+  }
+  for (int j = 0; j < kEnvReal; ++j) a.st.env[j][env] = T(0);
+  a.st.ep_step[env] = 0;
+  a.st.event[env] = 0;
+  a.st.episodes[env] = 0;
+}
+
+// =======================================================================================
+// host side
+// =======================================================================================
+struct sit_handle {
+  int precision = SIT_F32;
+  int n_env = 0;
+  int cap = 0;
+  int device = 0;
+  sit_params p{};
+  std::string err;
+  // state blob
+  unsigned char* blob = nullptr;
+  size_t blob_bytes = 0;
+  size_t off[kNumFields] = {};
+  int64_t count[kNumFields] = {};
+  // scenario
+  unsigned char* scen = nullptr;
+  size_t scen_init = 0, scen_end_n = 0, scen_end_e = 0, scen_nw0 = 0, scen_ab_len = 0,
+         scen_ab_alpha = 0, scen_initial = 0, scen_bytes = 0;
+  // map
+  unsigned char* map = nullptr;
+  int n_poly = 0, n_vert = 0;
+  size_t map_off = 0, map_vx = 0, map_vy = 0, map_nxt = 0, map_il2 = 0, map_bbox = 0;
+  double min_n = 0, max_n = 0, min_e = 0, max_e = 0;
+  bool have_map = false, have_routes = false, have_init = false;
+};
+
+namespace {
+
+thread_local std::string g_create_err;
+
+int fail(sit_handle* h, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (h) h->err = buf; else g_create_err = buf;
+  return code;
+}
+
+#define HIP_TRY(h, call)                                                                    \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess) return fail((h), SIT_E_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+size_t real_size(const sit_handle* h) { return h->precision == SIT_F64 ? 8 : 4; }
+
+// Derived constants, computed like the reference constructors (ship_model.py:71-130,
+// ship_engine.py:32-44, 316-325; controllers; MSRL_env_ex.py).
+template <typename T>
+Consts<T> make_consts(const sit_handle* h) {
+  const sit_params& p = h->p;
+  Consts<T> c{};
+  const double dwt = p.dead_weight_tonnage;
+  const double payload = 0.9 * (dwt - p.bunkers);
+  const double lsw = dwt / p.coefficient_of_deadweight_to_displacement - dwt;
+  const double mass = lsw + payload + p.bunkers + p.ballast;
+  const double l = p.length_of_ship, w = p.width_of_ship;
+  const double i_z = mass * (l * l + w * w) / 12;
+  const double x_du = mass * p.added_mass_coefficient_in_surge;
+  const double y_dv = mass * p.added_mass_coefficient_in_sway;
+  const double n_dr = i_z * p.added_mass_coefficient_in_yaw;
+  const double area_f = w * p.front_height, area_l = l * p.side_height;
+  c.dt = (T)p.integration_step;
+  c.mass = (T)mass; c.x_du = (T)x_du; c.y_dv = (T)y_dv;
+  c.inv_m11 = (T)(1.0 / (mass + x_du));
+  c.inv_m22 = (T)(1.0 / (mass + y_dv));
+  c.inv_m33 = (T)(1.0 / (i_z + n_dr));
+  c.d_u = (T)(mass / p.mass_over_linear_friction_coefficient_in_surge);
+  c.d_v = (T)(mass / p.mass_over_linear_friction_coefficient_in_sway);
+  c.d_r = (T)(i_z / p.mass_over_linear_friction_coefficient_in_yaw);
+  c.ku = (T)p.nonlinear_friction_coefficient_in_surge;
+  c.kv = (T)p.nonlinear_friction_coefficient_in_sway;
+  c.kr = (T)p.nonlinear_friction_coefficient_in_yaw;
+  c.vc_n = (T)p.current_velocity_component_from_north;
+  c.vc_e = (T)p.current_velocity_component_from_east;
+  c.wind_speed = (T)p.wind_speed;
+  c.wind_sin = (T)std::sin(p.wind_direction);
+  c.wind_cos = (T)std::cos(p.wind_direction);
+  c.wk_u = (T)(-0.5 * p.rho_air * p.cx * area_f);
+  c.wk_v = (T)(-0.5 * p.rho_air * p.cy * area_l);
+  c.wk_n = (T)(-p.rho_air * p.cn * area_l * l);
+  c.c_rv = (T)p.rudder_angle_to_sway_force_coefficient;
+  c.c_rr = (T)p.rudder_angle_to_yaw_force_coefficient;
+  c.rudder_max = (T)(p.max_rudder_angle_degrees * M_PI / 180);
+  const double me = p.main_engine_capacity, el = p.electrical_capacity, hotel = p.hotel_load;
+  double avail = 0, avail_me = 0, avail_el = 0;
+  if (hotel != 0.0) {   // BaseMachineryModel only sets the powers for a truthy hotel load
+    if (p.shaft_generator_state == SIT_SG_MOTOR) { avail = me + el - hotel; avail_me = me; avail_el = el - hotel; }
+    else if (p.shaft_generator_state == SIT_SG_GEN) { avail = me - hotel; avail_me = me - hotel; avail_el = 0; }
+    else { avail = me; avail_me = me; avail_el = 0; }
+  }
+  c.avail_prop = (T)avail; c.avail_me = (T)avail_me; c.avail_el = (T)avail_el;
+  c.tqcap_me = (T)(avail_me / 5 * M_PI / 30);
+  c.tqcap_el = (T)(avail_el / 5 * M_PI / 30);
+  c.d_me = (T)p.linear_friction_main_engine;
+  c.d_hsg = (T)p.linear_friction_hybrid_shaft_generator;
+  c.r_me = (T)p.gear_ratio_between_main_engine_and_propeller;
+  c.r_hsg = (T)p.gear_ratio_between_hybrid_shaft_generator_and_propeller;
+  c.kp_prop = (T)p.propeller_speed_to_torque_coefficient;
+  c.jp = (T)p.propeller_inertia;
+  c.thrust_k = (T)(std::pow(p.propeller_diameter, 4.0) * p.propeller_speed_to_thrust_force_coefficient);
+  c.me_cap = (T)me; c.hotel = (T)hotel; c.load_el_gen = (T)std::min(hotel, el);
+  c.sg_mode = p.shaft_generator_state;
+  c.collision_bias = p.collision_bias;
+  c.kp1 = (T)p.kp_ship_speed; c.ki1 = (T)p.ki_ship_speed;
+  c.kp2 = (T)p.kp_shaft_speed; c.ki2 = (T)p.ki_shaft_speed;
+  c.kp_h = (T)p.heading_kp; c.kd_h = (T)p.heading_kd; c.ki_h = (T)p.heading_ki;
+  c.los_r = (T)p.lookahead_distance;
+  c.los_r2 = (T)(p.lookahead_distance * p.lookahead_distance);
+  c.los_clamp = (T)(0.99 * p.lookahead_distance);
+  c.los_ki = (T)p.los_integral_gain;
+  c.windup = (T)p.integrator_windup_limit;
+  c.ra2 = p.radius_of_acceptance * p.radius_of_acceptance;
+  c.bias_scale = (T)p.bias_throttle_scale;
+  c.bias_max = (T)p.bias_throttle_max;
+  c.bias_rudder = (T)(p.bias_rudder_degrees * (M_PI / 180.0));
+  c.e_tol = (T)p.e_tolerance;
+  c.arrival_radius = (T)p.arrival_radius;
+  c.rpm_max = (T)p.shaft_rpm_max;
+  c.min_dist2 = (T)(p.minimum_ship_distance * p.minimum_ship_distance);
+  c.theta = (T)p.theta;
+  c.blackout_kw = (T)(me / 1000);
+  c.rpm_k = (T)(30.0 / M_PI);
+  c.half_len = (T)(l / 2);
+  c.min_n = (T)h->min_n; c.max_n = (T)h->max_n; c.min_e = (T)h->min_e; c.max_e = (T)h->max_e;
+  c.pi6 = (T)(M_PI / 6.0);
+  return c;
+}
+
+template <typename T>
+KArgs<T> make_args(const sit_handle* h) {
+  KArgs<T> a{};
+  a.c = make_consts<T>(h);
+  a.n_env = h->n_env;
+  a.cap = h->cap;
+  auto fp = [&](int f) { return reinterpret_cast<T*>(h->blob + h->off[f]); };
+  auto ip = [&](int f) { return reinterpret_cast<int32_t*>(h->blob + h->off[f]); };
+  for (int i = 0; i < kShipReal; ++i) a.st.ship[i] = fp(F_NORTH + i);
+  a.st.k = ip(F_K); a.st.nw = ip(F_NW); a.st.ticks = ip(F_TICKS); a.st.stop = ip(F_STOP);
+  for (int i = 0; i < kEnvReal; ++i) a.st.env[i] = fp(F_SAMP + i);
+  a.st.ep_step = ip(F_EP);
+  a.st.event = reinterpret_cast<uint32_t*>(h->blob + h->off[F_EVENT]);
+  a.st.episodes = reinterpret_cast<uint32_t*>(h->blob + h->off[F_EPISODES]);
+  a.st.wn = fp(F_WN); a.st.we = fp(F_WE);
+  a.sc.init = reinterpret_cast<const T*>(h->scen + h->scen_init);
+  a.sc.end_n = reinterpret_cast<const T*>(h->scen + h->scen_end_n);
+  a.sc.end_e = reinterpret_cast<const T*>(h->scen + h->scen_end_e);
+  a.sc.nw0 = reinterpret_cast<const int32_t*>(h->scen + h->scen_nw0);
+  a.sc.ab_len = reinterpret_cast<const double*>(h->scen + h->scen_ab_len);
+  a.sc.ab_alpha = reinterpret_cast<const double*>(h->scen + h->scen_ab_alpha);
+  a.sc.initial_state = reinterpret_cast<const T*>(h->scen + h->scen_initial);
+  a.map.n_poly = h->n_poly;
+  a.map.off = reinterpret_cast<const int32_t*>(h->map + h->map_off);
+  a.map.vx = reinterpret_cast<const T*>(h->map + h->map_vx);
+  a.map.vy = reinterpret_cast<const T*>(h->map + h->map_vy);
+  a.map.nxt = reinterpret_cast<const int32_t*>(h->map + h->map_nxt);
+  a.map.inv_len2 = reinterpret_cast<const T*>(h->map + h->map_il2);
+  a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
+  return a;
+}
+
+int ready(sit_handle* h) {
+  if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
+  if (!h->have_map) return fail(h, SIT_E_STATE, "sit_load_map has not been called");
+  if (!h->have_routes) return fail(h, SIT_E_STATE, "sit_load_routes has not been called");
+  if (!h->have_init) return fail(h, SIT_E_STATE, "sit_load_initial has not been called");
+  return SIT_OK;
+}
+
+template <typename T>
+size_t stage_lds_bytes(const sit_handle* h) { return (size_t)2 * 2 * h->cap * kWave * sizeof(T); }
+
+template <typename T>
+int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
+  KArgs<T> a = make_args<T>(h);
+  a.io = io;
+  const int blocks = (h->n_env + kEnvsPerBlock - 1) / kEnvsPerBlock;
+  const bool synth = io.action_ne == nullptr;
+  const size_t lds = stage_lds_bytes<T>(h);
+  const bool stage = io.n_steps > 1 && lds <= 96 * 1024;
+  if (stage) {
+    if (synth)
+      HIP_TRY(h, hipFuncSetAttribute((const void*)k_env_steps<T, true, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    else
+      HIP_TRY(h, hipFuncSetAttribute((const void*)k_env_steps<T, false, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  }
+  if (synth && stage)
+    hipLaunchKernelGGL((k_env_steps<T, true, true>), dim3(blocks), dim3(128), lds, stream, a);
+  else if (synth)
+    hipLaunchKernelGGL((k_env_steps<T, true, false>), dim3(blocks), dim3(128), 0, stream, a);
+  else if (stage)
+    hipLaunchKernelGGL((k_env_steps<T, false, true>), dim3(blocks), dim3(128), lds, stream, a);
+  else
+    hipLaunchKernelGGL((k_env_steps<T, false, false>), dim3(blocks), dim3(128), 0, stream, a);
+  HIP_TRY(h, hipGetLastError());
+  return SIT_OK;
+}
+
+}  // namespace
+
+// =======================================================================================
+// C ABI
+// =======================================================================================
+extern "C" {
+
+int32_t sit_abi_version(void) { return SIT_ABI_VERSION; }
+size_t sit_params_size(void) { return sizeof(sit_params); }
+
+void sit_params_default(sit_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  // test_beds/test_policy.py:102-124
+  p->dead_weight_tonnage = 3850000;
+  p->coefficient_of_deadweight_to_displacement = 0.7;
+  p->bunkers = 200000;
+  p->ballast = 200000;
+  p->length_of_ship = 80;
+  p->width_of_ship = 16;
+  p->added_mass_coefficient_in_surge = 0.4;
+  p->added_mass_coefficient_in_sway = 0.4;
+  p->added_mass_coefficient_in_yaw = 0.4;
+  p->mass_over_linear_friction_coefficient_in_surge = 130;
+  p->mass_over_linear_friction_coefficient_in_sway = 18;
+  p->mass_over_linear_friction_coefficient_in_yaw = 90;
+  p->nonlinear_friction_coefficient_in_surge = 2400;
+  p->nonlinear_friction_coefficient_in_sway = 4000;
+  p->nonlinear_friction_coefficient_in_yaw = 400;
+  p->current_velocity_component_from_north = -2;
+  p->current_velocity_component_from_east = -2;
+  p->wind_speed = 2;
+  p->wind_direction = -M_PI / 4;
+  // ship_model.py:123-130
+  p->rho_air = 1.2; p->front_height = 8.0; p->side_height = 8.0;
+  p->cx = 0.5; p->cy = 0.7; p->cn = 0.08;
+  p->integration_step = 0.5;
+  // test_policy.py:132-168 (PTI mode)
+  p->hotel_load = 200000;
+  p->main_engine_capacity = 0;
+  p->electrical_capacity = 2 * 510e3;
+  p->shaft_generator_state = SIT_SG_MOTOR;
+  p->rated_speed_main_engine_rpm = 1000;
+  p->linear_friction_main_engine = 68;
+  p->linear_friction_hybrid_shaft_generator = 57;
+  p->gear_ratio_between_main_engine_and_propeller = 0.6;
+  p->gear_ratio_between_hybrid_shaft_generator_and_propeller = 0.6;
+  p->propeller_inertia = 6000;
+  p->propeller_speed_to_torque_coefficient = 7.5;
+  p->propeller_diameter = 3.1;
+  p->propeller_speed_to_thrust_force_coefficient = 1.7;
+  p->rudder_angle_to_sway_force_coefficient = 50e3;
+  p->rudder_angle_to_yaw_force_coefficient = 500e3;
+  p->max_rudder_angle_degrees = 30;
+  // test_policy.py:199-217
+  p->kp_ship_speed = 7; p->ki_ship_speed = 0.13; p->kp_shaft_speed = 0.05; p->ki_shaft_speed = 0.005;
+  p->heading_kp = 1; p->heading_kd = 90; p->heading_ki = 0.01;
+  p->radius_of_acceptance = 300; p->lookahead_distance = 1000;
+  p->los_integral_gain = 0.002; p->integrator_windup_limit = 4000;
+  // test_policy.py:39-42; MSRL_env_ex.py:119, 557, 592, 754; MSRL_Env.py:246-250
+  p->theta = 2; p->sampling_frequency = 7; p->collision_bias = 1;
+  p->e_tolerance = 1000; p->arrival_radius = 200; p->shaft_rpm_max = 2000; p->minimum_ship_distance = 50;
+  p->bias_throttle_scale = 0.5; p->bias_throttle_max = 1.1; p->bias_rudder_degrees = 3;
+}
+
+const char* sit_last_error(const sit_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
+int32_t sit_precision(const sit_handle* h) { return h ? h->precision : 0; }
+int32_t sit_n_env(const sit_handle* h) { return h ? h->n_env : 0; }
+int32_t sit_state_nfields(void) { return kNumFields; }
+
+int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t precision, sit_handle** out) {
+  if (!p || !out) return fail(nullptr, SIT_E_INVALID, "null argument");
+  *out = nullptr;
+  if (n_env <= 0) return fail(nullptr, SIT_E_INVALID, "n_env must be positive (got %d)", n_env);
+  if (wpt_capacity < 2 || wpt_capacity > 1024)
+    return fail(nullptr, SIT_E_INVALID, "wpt_capacity must be in [2, 1024] (got %d)", wpt_capacity);
+  if (precision != SIT_F32 && precision != SIT_F64)
+    return fail(nullptr, SIT_E_INVALID, "precision must be SIT_F32 or SIT_F64 (got %d)", precision);
+  if (p->integration_step <= 0 || p->sampling_frequency <= 0 || p->lookahead_distance <= 0)
+    return fail(nullptr, SIT_E_INVALID, "integration_step, sampling_frequency and lookahead_distance must be positive");
+  if (p->shaft_generator_state < SIT_SG_MOTOR || p->shaft_generator_state > SIT_SG_OFF)
+    return fail(nullptr, SIT_E_INVALID, "shaft_generator_state out of range");
+  sit_handle* h = new sit_handle();
+  h->precision = precision;
+  h->n_env = n_env;
+  h->cap = wpt_capacity;
+  h->p = *p;
+  hipError_t e = hipGetDevice(&h->device);
+  if (e != hipSuccess) { fail(nullptr, SIT_E_HIP, "hipGetDevice: %s", hipGetErrorString(e)); delete h; return SIT_E_HIP; }
+  const size_t rs = real_size(h);
+  size_t off = 0;
+  for (int f = 0; f < kNumFields; ++f) {
+    int64_t cnt = kFields[f].extent == kShip ? 2LL * n_env
+                 : kFields[f].extent == kEnv ? (int64_t)n_env : 2LL * wpt_capacity * n_env;
+    const size_t el = kFields[f].dtype == SIT_DT_REAL ? rs : 4;
+    h->off[f] = off;
+    h->count[f] = cnt;
+    off = align256(off + (size_t)cnt * el);
+  }
+  h->blob_bytes = off;
+  // scenario
+  size_t so = 0;
+  h->scen_init = so; so = align256(so + (size_t)2 * SIT_INIT_NF * n_env * rs);
+  h->scen_end_n = so; so = align256(so + (size_t)2 * n_env * rs);
+  h->scen_end_e = so; so = align256(so + (size_t)2 * n_env * rs);
+  h->scen_nw0 = so; so = align256(so + (size_t)2 * n_env * 4);
+  h->scen_ab_len = so; so = align256(so + (size_t)n_env * 8);
+  h->scen_ab_alpha = so; so = align256(so + (size_t)n_env * 8);
+  h->scen_initial = so; so = align256(so + (size_t)n_env * SIT_OBS_DIM * rs);
+  h->scen_bytes = so;
+  if (hipMalloc(&h->blob, h->blob_bytes) != hipSuccess || hipMalloc(&h->scen, h->scen_bytes) != hipSuccess) {
+    fail(nullptr, SIT_E_NOMEM, "hipMalloc of %zu + %zu bytes failed", h->blob_bytes, h->scen_bytes);
+    sit_destroy(h);
+    return SIT_E_NOMEM;
+  }
+  if (hipMemset(h->blob, 0, h->blob_bytes) != hipSuccess || hipMemset(h->scen, 0, h->scen_bytes) != hipSuccess) {
+    fail(nullptr, SIT_E_HIP, "hipMemset failed");
+    sit_destroy(h);
+    return SIT_E_HIP;
+  }
+  *out = h;
+  return SIT_OK;
+}
+
+void sit_destroy(sit_handle* h) {
+  if (!h) return;
+  if (h->blob) (void)hipFree(h->blob);
+  if (h->scen) (void)hipFree(h->scen);
+  if (h->map) (void)hipFree(h->map);
+  delete h;
+}
+
+int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, const double* verts_en) {
+  if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
+  if (n_poly <= 0 || n_poly > kMaxPolys || !vert_offsets || !verts_en)
+    return fail(h, SIT_E_INVALID, "need 1..%d polygons with offsets and vertices", kMaxPolys);
+  if (vert_offsets[0] != 0) return fail(h, SIT_E_INVALID, "vert_offsets[0] must be 0");
+  for (int p = 0; p < n_poly; ++p)
+    if (vert_offsets[p + 1] - vert_offsets[p] < 3) return fail(h, SIT_E_INVALID, "polygon %d has < 3 vertices", p);
+  const int nv = vert_offsets[n_poly];
+  if (nv > kMaxPolyVerts) return fail(h, SIT_E_INVALID, "at most %d vertices (got %d)", kMaxPolyVerts, nv);
+  const size_t rs = real_size(h);
+  std::vector<double> vx(nv), vy(nv), il2(nv), bbox(4 * n_poly);
+  std::vector<int32_t> nxt(nv), offs(vert_offsets, vert_offsets + n_poly + 1);
+  // PolygonObstacle.map_boundaries (obstacle.py:111-124): vertices are (east, north)
+  h->min_e = h->min_n = INFINITY;
+  h->max_e = h->max_n = -INFINITY;
+  for (int p = 0; p < n_poly; ++p) {
+    double bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
+    for (int i = offs[p]; i < offs[p + 1]; ++i) {
+      vx[i] = verts_en[2 * i];
+      vy[i] = verts_en[2 * i + 1];
+      nxt[i] = (i + 1 < offs[p + 1]) ? i + 1 : offs[p];
+      bx0 = std::min(bx0, vx[i]); bx1 = std::max(bx1, vx[i]);
+      by0 = std::min(by0, vy[i]); by1 = std::max(by1, vy[i]);
+    }
+    bbox[4 * p + 0] = bx0; bbox[4 * p + 1] = bx1; bbox[4 * p + 2] = by0; bbox[4 * p + 3] = by1;
+    h->min_e = std::min(h->min_e, bx0); h->max_e = std::max(h->max_e, bx1);
+    h->min_n = std::min(h->min_n, by0); h->max_n = std::max(h->max_n, by1);
+  }
+  for (int i = 0; i < nv; ++i) {
+    const double ex = vx[nxt[i]] - vx[i], ey = vy[nxt[i]] - vy[i];
+    const double l2 = ex * ex + ey * ey;
+    il2[i] = l2 > 0 ? 1.0 / l2 : 0.0;
+  }
+  size_t o = 0;
+  h->map_off = o; o = align256(o + (n_poly + 1) * 4);
+  h->map_vx = o; o = align256(o + nv * rs);
+  h->map_vy = o; o = align256(o + nv * rs);
+  h->map_nxt = o; o = align256(o + nv * 4);
+  h->map_il2 = o; o = align256(o + nv * rs);
+  h->map_bbox = o; o = align256(o + 4 * n_poly * rs);
+  std::vector<unsigned char> host(o, 0);
+  std::memcpy(host.data() + h->map_off, offs.data(), (n_poly + 1) * 4);
+  std::memcpy(host.data() + h->map_nxt, nxt.data(), nv * 4);
+  auto put = [&](size_t at, const std::vector<double>& src) {
+    for (size_t i = 0; i < src.size(); ++i) {
+      if (rs == 8) reinterpret_cast<double*>(host.data() + at)[i] = src[i];
+      else reinterpret_cast<float*>(host.data() + at)[i] = (float)src[i];
+    }
+  };
+  put(h->map_vx, vx); put(h->map_vy, vy); put(h->map_il2, il2); put(h->map_bbox, bbox);
+  if (h->map) { (void)hipFree(h->map); h->map = nullptr; }
+  HIP_TRY(h, hipMalloc(&h->map, o));
+  HIP_TRY(h, hipMemcpy(h->map, host.data(), o, hipMemcpyHostToDevice));
+  h->n_poly = n_poly;
+  h->n_vert = nv;
+  h->have_map = true;
+  return SIT_OK;
+}
+
+int sit_load_routes(sit_handle* h, const double* wpt_ne, const int32_t* n_wpt) {
+  if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
+  if (!wpt_ne || !n_wpt) return fail(h, SIT_E_INVALID, "null route arrays");
+  const int n = h->n_env, cap = h->cap;
+  const size_t rs = real_size(h);
+  std::vector<double> tab((size_t)2 * 2 * cap * n, 0.0), end((size_t)2 * 2 * n), ab_len(n), ab_alpha(n);
+  std::vector<int32_t> nw0((size_t)2 * n);
+  for (int e = 0; e < n; ++e) {
+    for (int t = 0; t < 2; ++t) {
+      const int nw = n_wpt[2 * e + t];
+      if (nw < 2 || nw > cap) return fail(h, SIT_E_INVALID, "env %d ship %d: n_wpt %d not in [2, %d]", e, t, nw, cap);
+      const double* r = wpt_ne + ((size_t)(e * 2 + t) * cap) * 2;
+      for (int i = 0; i < nw - 1; ++i) {
+        tab[((size_t)(0 * 2 + t) * cap + i) * n + e] = r[2 * i];
+        tab[((size_t)(1 * 2 + t) * cap + i) * n + e] = r[2 * i + 1];
+      }
+      end[(size_t)(0 * 2 + t) * n + e] = r[2 * (nw - 1)];
+      end[(size_t)(1 * 2 + t) * n + e] = r[2 * (nw - 1) + 1];
+      nw0[(size_t)t * n + e] = nw;
+      if (t == 1) {   // reward_function_params (MSRL_Env.py:119-128)
+        const double dn = r[2 * (nw - 1)] - r[0], de = r[2 * (nw - 1) + 1] - r[1];
+        ab_len[e] = std::sqrt(dn * dn + de * de) / h->p.sampling_frequency;
+        ab_alpha[e] = std::atan2(de, dn);
+      }
+    }
+  }
+  auto conv = [&](const double* src, size_t cnt) {
+    std::vector<unsigned char> out(cnt * rs);
+    for (size_t i = 0; i < cnt; ++i) {
+      if (rs == 8) reinterpret_cast<double*>(out.data())[i] = src[i];
+      else reinterpret_cast<float*>(out.data())[i] = (float)src[i];
+    }
+    return out;
+  };
+  const size_t tcnt = (size_t)2 * cap * n;
+  auto tn = conv(tab.data(), tcnt), te = conv(tab.data() + tcnt, tcnt);
+  auto en = conv(end.data(), (size_t)2 * n), ee = conv(end.data() + (size_t)2 * n, (size_t)2 * n);
+  HIP_TRY(h, hipMemcpy(h->blob + h->off[F_WN], tn.data(), tn.size(), hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemcpy(h->blob + h->off[F_WE], te.data(), te.size(), hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemcpy(h->scen + h->scen_end_n, en.data(), en.size(), hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemcpy(h->scen + h->scen_end_e, ee.data(), ee.size(), hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemcpy(h->scen + h->scen_nw0, nw0.data(), nw0.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemcpy(h->scen + h->scen_ab_len, ab_len.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemcpy(h->scen + h->scen_ab_alpha, ab_alpha.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+  h->have_routes = true;
+  return SIT_OK;
+}
+
+int sit_load_initial(sit_handle* h, const double* init) {
+  if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
+  if (!init) return fail(h, SIT_E_INVALID, "null init array");
+  const int n = h->n_env;
+  const size_t rs = real_size(h);
+  std::vector<double> sc((size_t)2 * SIT_INIT_NF * n), ist((size_t)n * SIT_OBS_DIM, 0.0);
+  for (int e = 0; e < n; ++e)
+    for (int t = 0; t < 2; ++t)
+      for (int f = 0; f < SIT_INIT_NF; ++f)
+        sc[((size_t)t * SIT_INIT_NF + f) * n + e] = init[((size_t)e * 2 + t) * SIT_INIT_NF + f];
+  // construction-time observation, rounded to float32 as the reference's array (MSRL_Env.py:88-91)
+  for (int e = 0; e < n; ++e) {
+    const double* a = init + (size_t)e * 2 * SIT_INIT_NF;
+    const double* b = a + SIT_INIT_NF;
+    double* o = &ist[(size_t)e * SIT_OBS_DIM];
+    o[0] = (float)a[SIT_INIT_NORTH]; o[1] = (float)a[SIT_INIT_EAST]; o[2] = (float)a[SIT_INIT_YAW];
+    o[6] = (float)b[SIT_INIT_NORTH]; o[7] = (float)b[SIT_INIT_EAST]; o[8] = (float)b[SIT_INIT_YAW];
+  }
+  auto conv = [&](const std::vector<double>& src) {
+    std::vector<unsigned char> out(src.size() * rs);
+    for (size_t i = 0; i < src.size(); ++i) {
+      if (rs == 8) reinterpret_cast<double*>(out.data())[i] = src[i];
+      else reinterpret_cast<float*>(out.data())[i] = (float)src[i];
+    }
+    return out;
+  };
+  auto a = conv(sc), b = conv(ist);
+  HIP_TRY(h, hipMemcpy(h->scen + h->scen_init, a.data(), a.size(), hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemcpy(h->scen + h->scen_initial, b.data(), b.size(), hipMemcpyHostToDevice));
+  h->have_init = true;
+  return SIT_OK;
+}
+
+int sit_restart(sit_handle* h, void* stream) {
+  int rc = ready(h);
+  if (rc) return rc;
+  const int blocks = (h->n_env + 255) / 256;
+  if (h->precision == SIT_F64)
+    hipLaunchKernelGGL(k_restart<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, make_args<double>(h));
+  else
+    hipLaunchKernelGGL(k_restart<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, make_args<float>(h));
+  HIP_TRY(h, hipGetLastError());
+  return SIT_OK;
+}
+
+int sit_reset(sit_handle* h, const uint8_t* env_mask, void* initial_state, void* stream) {
+  int rc = ready(h);
+  if (rc) return rc;
+  const int blocks = (h->n_env + 255) / 256;
+  if (h->precision == SIT_F64)
+    hipLaunchKernelGGL(k_reset<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, make_args<double>(h),
+                       env_mask, (double*)initial_state);
+  else
+    hipLaunchKernelGGL(k_reset<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, make_args<float>(h),
+                       env_mask, (float*)initial_state);
+  HIP_TRY(h, hipGetLastError());
+  return SIT_OK;
+}
+
+int sit_init_step(sit_handle* h, const uint8_t* env_mask, void* stream) {
+  int rc = ready(h);
+  if (rc) return rc;
+  const int blocks = (2 * h->n_env + 255) / 256;
+  if (h->precision == SIT_F64)
+    hipLaunchKernelGGL(k_init_step<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, make_args<double>(h), env_mask);
+  else
+    hipLaunchKernelGGL(k_init_step<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, make_args<float>(h), env_mask);
+  HIP_TRY(h, hipGetLastError());
+  return SIT_OK;
+}
+
+int sit_step(sit_handle* h, const void* action_ne, const uint8_t* sac_update, const uint8_t* init,
+             void* next_state, void* reward, uint8_t* done, uint32_t* status, int32_t* done_count,
+             void* stream) {
+  int rc = ready(h);
+  if (rc) return rc;
+  if (!action_ne || !sac_update || !init) return fail(h, SIT_E_INVALID, "action_ne, sac_update and init are required");
+  if (!next_state && !reward) return fail(h, SIT_E_INVALID, "need next_state or reward output");
+  if (h->precision == SIT_F64) {
+    StepIO<double> io{};
+    io.n_steps = 1; io.action_ne = (const double*)action_ne; io.sac_update = sac_update; io.init = init;
+    io.next_state = (double*)next_state; io.reward = (double*)reward; io.done = done; io.status = status;
+    io.done_count = done_count;
+    return launch_steps<double>(h, io, (hipStream_t)stream);
+  }
+  StepIO<float> io{};
+  io.n_steps = 1; io.action_ne = (const float*)action_ne; io.sac_update = sac_update; io.init = init;
+  io.next_state = (float*)next_state; io.reward = (float*)reward; io.done = done; io.status = status;
+  io.done_count = done_count;
+  return launch_steps<float>(h, io, (hipStream_t)stream);
+}
+
+int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
+  int rc = ready(h);
+  if (rc) return rc;
+  if (!ra) return fail(h, SIT_E_INVALID, "null rollout args");
+  if (ra->n_steps <= 0) return fail(h, SIT_E_INVALID, "n_steps must be positive");
+  if (!ra->next_state && !ra->reward) return fail(h, SIT_E_INVALID, "need next_state or reward output");
+  if (ra->action_ne && (!ra->sac_update || !ra->init))
+    return fail(h, SIT_E_INVALID, "explicit actions need sac_update and init");
+  if (ra->env_id_offset < 0) return fail(h, SIT_E_INVALID, "env_id_offset must be >= 0");
+  auto fill = [&](auto* io, auto* tag) {
+    using R = std::remove_pointer_t<decltype(tag)>;
+    io->n_steps = ra->n_steps; io->auto_reset = ra->auto_reset; io->seed = ra->seed;
+    io->env_id_offset = ra->env_id_offset;
+    io->action_ne = (const R*)ra->action_ne; io->sac_update = ra->sac_update; io->init = ra->init;
+    io->next_state = (R*)ra->next_state; io->reward = (R*)ra->reward; io->done = ra->done;
+    io->status = ra->status; io->action_out = (R*)ra->action_out; io->done_count = ra->done_count;
+  };
+  if (h->precision == SIT_F64) {
+    StepIO<double> io{};
+    fill(&io, (double*)nullptr);
+    return launch_steps<double>(h, io, (hipStream_t)stream);
+  }
+  StepIO<float> io{};
+  fill(&io, (float*)nullptr);
+  return launch_steps<float>(h, io, (hipStream_t)stream);
+}
+
+int sit_state_field(const sit_handle* h, int32_t id, const char** name, size_t* offset, int32_t* dtype,
+                    int64_t* count) {
+  if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
+  if (id < 0 || id >= kNumFields) return SIT_E_INVALID;
+  if (name) *name = kFields[id].name;
+  if (offset) *offset = h->off[id];
+  if (dtype) *dtype = kFields[id].dtype;
+  if (count) *count = h->count[id];
+  return SIT_OK;
+}
+
+int sit_state_bytes(const sit_handle* h, size_t* bytes) {
+  if (!h || !bytes) return fail(nullptr, SIT_E_INVALID, "null argument");
+  *bytes = h->blob_bytes;
+  return SIT_OK;
+}
+
+int sit_get_state(sit_handle* h, void* dst, void* stream) {
+  if (!h || !dst) return fail(h, SIT_E_INVALID, "null argument");
+  HIP_TRY(h, hipMemcpyAsync(dst, h->blob, h->blob_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return SIT_OK;
+}
+
+int sit_set_state(sit_handle* h, const void* src, void* stream) {
+  if (!h || !src) return fail(h, SIT_E_INVALID, "null argument");
+  HIP_TRY(h, hipMemcpyAsync(h->blob, src, h->blob_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return SIT_OK;
+}
+
+}  // extern "C"

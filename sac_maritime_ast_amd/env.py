@@ -1,0 +1,233 @@
+"""Batched two-ship environment on one MI355X: ``VecMultiShipRLEnv``.
+
+N independent copies of the reference's ``MultiShipRLEnv`` (RLEnv/MSRL_Env.py:37-450 with the
+reward/termination of RLEnv/MSRL_env_ex.py:450-980) stepped by the HIP kernels of libsit.so.
+All per-step tensors live on the GPU; PyTorch is used only for device memory and streams.
+
+Method              reference counterpart
+  reset(mask)         MultiShipRLEnv.reset        MSRL_Env.py:147-188
+  init_step(mask)     MultiShipRLEnv.init_step    MSRL_Env.py:190-217
+  step(a, sac, init)  MultiShipRLEnv.step         MSRL_Env.py:404-442
+  rollout(K, seed)    K steps of test_beds/main_ast.py:310-412 with the synthetic sampler
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_char_p, c_int32, c_int64, c_size_t, c_void_p
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import params as default_params
+from .scenario import Scenario, make_scenario
+
+
+def _ptr(t):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+class VecMultiShipRLEnv:
+    """N two-ship environments resident in HBM.
+
+    precision 32 (default, BASELINE fp32) or 64 (bit-faithful float64 arithmetic of the reference).
+    """
+
+    def __init__(self, n_env: int | None = None, scenario: Scenario | None = None, params=None,
+                 precision: int = 32, wpt_capacity: int = 32, device=None):
+        if scenario is None:
+            if n_env is None:
+                raise ValueError("give n_env or a scenario")
+            scenario = make_scenario(n_env, cap=wpt_capacity)
+        self.scenario = scenario
+        self.n_env = int(scenario.n_env)
+        self.cap = int(scenario.routes.shape[2])
+        if precision not in (32, 64):
+            raise ValueError("precision must be 32 or 64")
+        self.precision = precision
+        self.dtype = torch.float32 if precision == 32 else torch.float64
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise ValueError("VecMultiShipRLEnv runs on a ROCm GPU device")
+        self.params = params if params is not None else default_params()
+        self.lib = _lib.load()
+        self.handle = c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.sit_create(byref(self.params), self.n_env, self.cap, precision,
+                                           byref(self.handle)))
+            self._load(scenario)
+            self._call("sit_restart", self._stream())
+        self._layout = self._read_layout()
+        self._zero_i32 = None
+
+    # ---------------- plumbing ----------------
+    def _stream(self):
+        return c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _call(self, name, *args):
+        return _lib.check(getattr(self.lib, name)(self.handle, *args), self.handle)
+
+    def _load(self, sc: Scenario):
+        polys = [np.ascontiguousarray(p, dtype=np.float64) for p in sc.polys]
+        offs = np.zeros(len(polys) + 1, dtype=np.int32)
+        offs[1:] = np.cumsum([len(p) for p in polys])
+        verts = np.ascontiguousarray(np.concatenate(polys), dtype=np.float64)
+        self._call("sit_load_map", len(polys), offs.ctypes.data_as(c_void_p), verts.ctypes.data_as(c_void_p))
+        routes = np.ascontiguousarray(sc.routes, dtype=np.float64)
+        nw = np.ascontiguousarray(sc.n_wpt, dtype=np.int32)
+        self._call("sit_load_routes", routes.ctypes.data_as(c_void_p), nw.ctypes.data_as(c_void_p))
+        init = np.ascontiguousarray(sc.init, dtype=np.float64)
+        self._call("sit_load_initial", init.ctypes.data_as(c_void_p))
+
+    def _read_layout(self):
+        out = []
+        n = self.lib.sit_state_nfields()
+        for i in range(n):
+            name, off, dt, cnt = c_char_p(), c_size_t(), c_int32(), c_int64()
+            self._call("sit_state_field", i, byref(name), byref(off), byref(dt), byref(cnt))
+            out.append((name.value.decode(), off.value, dt.value, cnt.value))
+        nb = c_size_t()
+        self._call("sit_state_bytes", byref(nb))
+        self._state_bytes = nb.value
+        return out
+
+    def _field_shape(self, name, count):
+        if count == 2 * self.n_env:
+            return (2, self.n_env)
+        if count == self.n_env:
+            return (self.n_env,)
+        return (2, self.cap, self.n_env)
+
+    def _dev(self, t, dtype, shape, name):
+        if not isinstance(t, torch.Tensor):
+            t = torch.as_tensor(np.asarray(t))
+        if t.dtype == torch.bool:
+            t = t.to(torch.uint8)
+        t = t.to(device=self.device, dtype=dtype).reshape(shape).contiguous()
+        return t
+
+    def _mask(self, mask):
+        if mask is None:
+            return None
+        return self._dev(mask, torch.uint8, (self.n_env,), "mask")
+
+    # ---------------- env API ----------------
+    def restart(self):
+        """Construction-time state (as if freshly built)."""
+        with torch.cuda.device(self.device):
+            self._call("sit_restart", self._stream())
+
+    def reset(self, mask=None):
+        """MultiShipRLEnv.reset; returns the construction-time observation [n_env, 10]."""
+        out = torch.empty((self.n_env, _lib.SIT_OBS_DIM), dtype=self.dtype, device=self.device)
+        m = self._mask(mask)
+        with torch.cuda.device(self.device):
+            self._call("sit_reset", _ptr(m), _ptr(out), self._stream())
+        return out
+
+    def init_step(self, mask=None):
+        m = self._mask(mask)
+        with torch.cuda.device(self.device):
+            self._call("sit_init_step", _ptr(m), self._stream())
+
+    def step(self, action_ne, sac_update, init, done_count: torch.Tensor | None = None):
+        """One MultiShipRLEnv.step for every env.  Returns (next_state [n,10], reward [n],
+        done [n] bool, status [n] int64 bitmask)."""
+        n = self.n_env
+        a = self._dev(action_ne, self.dtype, (n, 2), "action_ne")
+        s = self._dev(sac_update, torch.uint8, (n,), "sac_update")
+        i = self._dev(init, torch.uint8, (n,), "init")
+        ns = torch.empty((n, _lib.SIT_OBS_DIM), dtype=self.dtype, device=self.device)
+        rew = torch.empty((n,), dtype=self.dtype, device=self.device)
+        done = torch.empty((n,), dtype=torch.uint8, device=self.device)
+        st = torch.empty((n,), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            self._call("sit_step", _ptr(a), _ptr(s), _ptr(i), _ptr(ns), _ptr(rew), _ptr(done), _ptr(st),
+                       _ptr(done_count), self._stream())
+        return ns, rew, done.bool(), st.to(torch.int64) & 0xFFFFFFFF
+
+    def rollout(self, n_steps: int, seed: int = 25450, auto_reset: bool = True, env_id_offset: int = 0,
+                actions: dict | None = None, out: dict | None = None, want=("next_state", "reward", "done",
+                                                                              "status", "action", "done_count")):
+        """K fused steps (one kernel launch).  actions=None: synthetic AST sampler on device.
+        Returns a dict of [K, n_env, ...] tensors (reused from `out` when given)."""
+        n, K = self.n_env, int(n_steps)
+        out = {} if out is None else out
+        shapes = {"next_state": ((K, n, _lib.SIT_OBS_DIM), self.dtype), "reward": ((K, n), self.dtype),
+                  "done": ((K, n), torch.uint8), "status": ((K, n), torch.int32),
+                  "action": ((K, n, 4), self.dtype), "done_count": ((K,), torch.int32)}
+        for k in want:
+            shp, dt = shapes[k]
+            t = out.get(k)
+            if t is None or tuple(t.shape) != shp or t.dtype != dt:
+                out[k] = torch.empty(shp, dtype=dt, device=self.device)
+        if "done_count" in out:
+            out["done_count"].zero_()
+        ra = _lib.RolloutArgs()
+        ra.n_steps, ra.auto_reset, ra.seed, ra.env_id_offset = K, int(bool(auto_reset)), int(seed), int(env_id_offset)
+        keep = []
+        if actions is not None:
+            a = self._dev(actions["action_ne"], self.dtype, (K, n, 2), "action_ne")
+            s = self._dev(actions["sac_update"], torch.uint8, (K, n), "sac_update")
+            i = self._dev(actions["init"], torch.uint8, (K, n), "init")
+            keep += [a, s, i]
+            ra.action_ne, ra.sac_update, ra.init = a.data_ptr(), s.data_ptr(), i.data_ptr()
+        for field, key in (("next_state", "next_state"), ("reward", "reward"), ("done", "done"),
+                           ("status", "status"), ("action_out", "action"), ("done_count", "done_count")):
+            t = out.get(key) if key in want else None
+            setattr(ra, field, None if t is None else t.data_ptr())
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.sit_rollout(self.handle, byref(ra), self._stream()), self.handle)
+        return out
+
+    # ---------------- state ----------------
+    def state_blob(self):
+        blob = torch.empty(self._state_bytes, dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            self._call("sit_get_state", _ptr(blob), self._stream())
+        return blob
+
+    def load_state_blob(self, blob):
+        if blob.numel() != self._state_bytes or blob.dtype != torch.uint8:
+            raise ValueError("state blob size/dtype mismatch")
+        blob = blob.to(self.device).contiguous()
+        with torch.cuda.device(self.device):
+            self._call("sit_set_state", _ptr(blob), self._stream())
+
+    def _views(self, blob):
+        views = {}
+        for name, off, dt, cnt in self._layout:
+            tdt = self.dtype if dt == _lib.SIT_DT_REAL else torch.int32
+            el = torch.tensor([], dtype=tdt).element_size()
+            v = blob[off:off + cnt * el].view(tdt).reshape(self._field_shape(name, cnt))
+            views[name] = v
+        return views
+
+    def get_state(self):
+        """Named tensors (copies): ship fields [2, n_env], env fields [n_env], route tables
+        [2, cap, n_env].  Unsigned fields are returned as int32."""
+        return self._views(self.state_blob())
+
+    def set_state(self, state: dict):
+        blob = self.state_blob()
+        views = self._views(blob)
+        for k, v in state.items():
+            if k not in views:
+                continue
+            views[k].copy_(torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v)
+                           .to(dtype=views[k].dtype, device=self.device).reshape(views[k].shape))
+        self.load_state_blob(blob)
+
+    def close(self):
+        if getattr(self, "handle", None) and self.handle.value:
+            self.lib.sit_destroy(self.handle)
+            self.handle = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_ = ctypes  # ctypes types are used through the _lib signatures

@@ -1,0 +1,77 @@
+"""Synthetic benchmark scenario.
+
+The reference's route files are referenced by absolute Windows paths and are not in the
+repository (test_beds/main_ast.py:221, test_beds/test_policy.py:210), so the benchmark uses
+synthetic routes validated against the island map of test_beds/test_policy.py:189-194:
+  test ship  R_test = [[1200,500],[1500,4500],[3500,7000],[7000,9000],[9500,9000]] (north, east)
+  obstacle   R_obs  = [[2200,5300],[8600,5200]] (start -> end pair, MSRL_env_ex.py:464)
+Initial state u = v = r = 0, shaft speed 400*pi/30, shaft-speed PI integral 114,
+desired speed 8.5 m/s; for N > 1 envs each ship's start is jittered by +-100 m and +-0.05 rad
+(numpy default_rng(seed)).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import INIT_FIELDS
+
+R_TEST = [[1200.0, 500.0], [1500.0, 4500.0], [3500.0, 7000.0], [7000.0, 9000.0], [9500.0, 9000.0]]
+R_OBS = [[2200.0, 5300.0], [8600.0, 5200.0]]
+# PolygonObstacle vertex lists, (east, north) tuples (test_beds/test_policy.py:189-194)
+ISLANDS = [
+    [(0, 10000), (5500, 10000), (5300, 9000), (4800, 8500), (4200, 7300), (4000, 5700), (4300, 4900),
+     (4900, 4400), (4400, 4000), (3200, 4100), (2000, 4500), (1000, 4000), (900, 3500), (500, 2600),
+     (0, 2350)],
+    [(10000, 0), (4000, 0), (4250, 250), (5000, 400), (6000, 900), (8000, 1100), (8500, 1500),
+     (9000, 2250), (9500, 3500), (10000, 4000)],
+    [(5500, 5500), (5700, 7000), (6200, 8100), (7500, 8000), (7800, 7000), (7600, 5500), (6900, 4700),
+     (6000, 5000)],
+    [(2000, 2000), (2500, 2300), (4000, 2500), (5000, 3000), (4200, 2100), (3400, 1900)],
+]
+OMEGA0 = 400 * math.pi / 30
+V_DES = 8.5
+SHAFT_PI_I0 = 114.0
+
+
+@dataclass
+class Scenario:
+    routes: np.ndarray   # float64[n_env, 2, cap, 2] (north, east)
+    n_wpt: np.ndarray    # int32[n_env, 2]
+    init: np.ndarray     # float64[n_env, 2, SIT_INIT_NF]
+    polys: list          # list of float64[m, 2] (east, north)
+
+    @property
+    def n_env(self):
+        return self.routes.shape[0]
+
+
+def polygons(islands=ISLANDS):
+    return [np.asarray(p, dtype=np.float64) for p in islands]
+
+
+def heading(a, b):
+    return math.atan2(b[1] - a[1], b[0] - a[0])
+
+
+def make_scenario(n_env: int, cap: int = 32, seed: int = 25450, jitter: bool = True,
+                  r_test=R_TEST, r_obs=R_OBS, v_des: float = V_DES) -> Scenario:
+    routes = np.zeros((n_env, 2, cap, 2))
+    routes[:, 0, :len(r_test)] = r_test
+    routes[:, 1, :len(r_obs)] = r_obs
+    n_wpt = np.zeros((n_env, 2), dtype=np.int32)
+    n_wpt[:, 0], n_wpt[:, 1] = len(r_test), len(r_obs)
+    init = np.zeros((n_env, 2, len(INIT_FIELDS)))
+    for t, r in enumerate((r_test, r_obs)):
+        init[:, t, 0], init[:, t, 1] = r[0]
+        init[:, t, 2] = heading(r[0], r[1])
+    init[:, :, 6] = OMEGA0
+    init[:, :, 7] = v_des
+    init[:, :, 9] = SHAFT_PI_I0
+    if jitter and n_env > 1:
+        rng = np.random.default_rng(seed)
+        init[:, :, 0:2] += rng.uniform(-100.0, 100.0, size=(n_env, 2, 2))
+        init[:, :, 2] += rng.uniform(-0.05, 0.05, size=(n_env, 2))
+    return Scenario(routes, n_wpt, init, polygons())

@@ -1,0 +1,106 @@
+"""CPU checks of the C-ABI library and the host-side package (no compute calls: no GPU here)."""
+import ctypes
+import os
+import re
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from helpers import ROOT
+from oracle import sit_oracle as so
+
+sit = pytest.importorskip("sac_maritime_ast_amd")
+from sac_maritime_ast_amd import _lib, config, scenario, status_string  # noqa: E402
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "sit.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sit_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 20
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in names if not hasattr(raw, n)]
+    assert not missing, f"missing exports: {missing}"
+    assert set(names) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/sit.h"
+    assert lib.sit_abi_version() == 1
+
+
+def test_params_layout_and_defaults_match_oracle():
+    lib = _lib.load()
+    assert lib.sit_params_size() == ctypes.sizeof(_lib.SitParams)
+    d = config.params().as_dict()
+    for k, v in so.DEFAULT_PARAMS.items():
+        assert d[k] == pytest.approx(v, rel=0, abs=0), k
+
+
+def test_create_without_device_fails_cleanly_or_succeeds():
+    """sit_create needs a HIP device; on a GPU-less host it must return an error, not crash."""
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    p = config.params()
+    rc = lib.sit_create(ctypes.byref(p), 4, 8, 32, ctypes.byref(h))
+    if rc == 0:
+        lib.sit_destroy(h)
+    else:
+        assert rc in (_lib.SIT_E_HIP, _lib.SIT_E_NOMEM)
+        assert lib.sit_last_error(None)
+
+
+def test_create_rejects_bad_arguments():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    p = config.params()
+    assert lib.sit_create(ctypes.byref(p), 0, 8, 32, ctypes.byref(h)) == _lib.SIT_E_INVALID
+    assert b"n_env" in lib.sit_last_error(None)
+    assert lib.sit_create(ctypes.byref(p), 4, 8, 16, ctypes.byref(h)) == _lib.SIT_E_INVALID
+    assert lib.sit_create(ctypes.byref(p), 4, 1, 32, ctypes.byref(h)) == _lib.SIT_E_INVALID
+
+
+def test_status_strings_match_oracle():
+    rng = np.random.default_rng(0)
+    for bits in [0, *rng.integers(0, 1 << 14, 500)]:
+        assert status_string(int(bits)) == so.status_string(int(bits))
+
+
+def test_params_from_reference_style_objects():
+    ship = SimpleNamespace(dead_weight_tonnage=3850000, coefficient_of_deadweight_to_displacement=0.7,
+                           bunkers=200000, ballast=200000, length_of_ship=80, width_of_ship=16,
+                           added_mass_coefficient_in_surge=0.4, added_mass_coefficient_in_sway=0.4,
+                           added_mass_coefficient_in_yaw=0.4, mass_over_linear_friction_coefficient_in_surge=130,
+                           mass_over_linear_friction_coefficient_in_sway=18,
+                           mass_over_linear_friction_coefficient_in_yaw=90,
+                           nonlinear_friction_coefficient__in_surge=2500,
+                           nonlinear_friction_coefficient__in_sway=4000, nonlinear_friction_coefficient__in_yaw=400)
+    mode = SimpleNamespace(main_engine_capacity=2160e3, electrical_capacity=0.0, shaft_generator_state="GEN")
+    mc = SimpleNamespace(hotel_load=200000, machinery_modes=SimpleNamespace(list_of_modes=[mode]),
+                         machinery_operating_mode=0, rated_speed_main_engine_rpm=1000,
+                         linear_friction_main_engine=68, linear_friction_hybrid_shaft_generator=57,
+                         gear_ratio_between_main_engine_and_propeller=0.6,
+                         gear_ratio_between_hybrid_shaft_generator_and_propeller=0.6, propeller_inertia=6000,
+                         propeller_speed_to_torque_coefficient=7.5, propeller_diameter=3.1,
+                         propeller_speed_to_thrust_force_coefficient=1.7,
+                         rudder_angle_to_sway_force_coefficient=50e3, rudder_angle_to_yaw_force_coefficient=500e3,
+                         max_rudder_angle_degrees=30)
+    p = config.params_from_reference(ship_config=ship, machinery_config=mc,
+                                     args=SimpleNamespace(sampling_frequency=9, theta=1.5))
+    assert p.nonlinear_friction_coefficient_in_surge == 2500
+    assert p.shaft_generator_state == _lib.SIT_SG_GEN and p.main_engine_capacity == 2160e3
+    assert p.sampling_frequency == 9 and p.theta == 1.5
+    assert config.shaft_speed_max(p) == pytest.approx(69.11503837897544)
+
+
+def test_scenario_matches_survey():
+    sc = scenario.make_scenario(1, jitter=False)
+    assert sc.init[0, 0, 2] == pytest.approx(1.4959364790841299, rel=1e-15)
+    assert sc.init[0, 1, 2] == pytest.approx(-0.015623728620476831, rel=1e-15)
+    big = scenario.make_scenario(4096)
+    d = big.init[:, :, :2] - sc.init[:, :, :2]
+    assert np.abs(d).max() <= 100.0 and np.abs(big.init[:, :, 2] - sc.init[:, :, 2]).max() <= 0.05
+    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+    assert o.ab_len[0] == pytest.approx(914.3973146174434, rel=1e-14)

@@ -1,0 +1,242 @@
+"""GPU parity: the HIP path (libsit.so through the C ABI) against the reference fixtures and the
+CPU oracle.  All tests here run on an MI355X (``-m gpu``).
+
+Contract:
+  * float64 handle: bit-faithful arithmetic order; teacher-forced and free-running results
+    within 1e-9 relative (per-field scale floors), waypoint index / stop flags / done / status
+    identical.  The remaining differences are ocml-vs-libm transcendental ulps.
+  * float32 handle: teacher-forced one step from float32-rounded states within 1e-5 relative
+    (per-field floors); discrete outputs identical except where the oracle's own decision
+    margin lies inside the float32 band (counted and bounded).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import (OBS_SCALE, POLYS, SCALE, env_oracle, env_state_all_rows, env_state_from, golden,
+                     golden_names, init_rows, params_for, rel_err)
+from oracle import sit_oracle as so
+
+pytestmark = pytest.mark.gpu
+
+sit = pytest.importorskip("sac_maritime_ast_amd")
+from sac_maritime_ast_amd import VecMultiShipRLEnv, make_scenario, status_string  # noqa: E402
+from sac_maritime_ast_amd.config import params as sit_params  # noqa: E402
+from sac_maritime_ast_amd.scenario import Scenario  # noqa: E402
+
+DEV = "cuda:0"
+TOL64 = 1e-9
+ENV_CASES = golden_names("env_")
+
+
+def gpu_params(mode_row=None, **over):
+    p = params_for(mode_row, **over)
+    kw = {k: v for k, v in p.items() if k in sit_params().as_dict()}
+    return sit_params(**kw)
+
+
+def fixture_env(d, n_env, precision):
+    sc = Scenario(np.repeat(d["routes"][None], n_env, 0), np.repeat(d["n_wpt"][None], n_env, 0).astype(np.int32),
+                  init_rows(np.repeat(d["pose"][None], n_env, 0)), POLYS)
+    return VecMultiShipRLEnv(scenario=sc, params=gpu_params(d["mode"]), precision=precision, device=DEV)
+
+
+def np_state(env):
+    return {k: v.cpu().numpy() for k, v in env.get_state().items()}
+
+
+def check_state(got, want, tol, where, int_fields=so.SHIP_INT, real_fields=so.SHIP_REAL):
+    for k in int_fields:
+        assert np.array_equal(got[k].astype(np.int64), np.asarray(want[k]).astype(np.int64)), f"{where}: {k}"
+    for k in real_fields:
+        err = rel_err(got[k], want[k], SCALE[k]).max()
+        assert err <= tol, f"{where}: {k} rel err {err:.3e}"
+
+
+# ------------------------------------------------------------------------------------------
+# float64: against the reference's own outputs
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ENV_CASES)
+def test_f64_teacher_forced_vs_reference(name):
+    d = golden(name)
+    T = len(d["reward"])
+    o = env_oracle(d, n_env=T)
+    st = env_state_all_rows(d, "pre_", o)
+    env = fixture_env(d, T, 64)
+    env.set_state(st)
+    act = np.stack([d["action_n"], d["action_e"]], axis=1)
+    ns, rew, done, status = env.step(act, d["sac_update"], d["init"])
+    ns, rew, done, status = ns.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy(), status.cpu().numpy()
+    assert rel_err(ns, d["next_state"], OBS_SCALE).max() <= TOL64
+    assert rel_err(rew, d["reward"], 1.0).max() <= TOL64
+    assert np.array_equal(done, d["done"].astype(bool))
+    for i in range(T):
+        assert status_string(int(status[i])) == str(d["status"][i]), f"{name} step {i}"
+    post = np_state(env)
+    want = {k: d["post_" + k].T for k in so.SHIP_REAL + so.SHIP_INT}
+    check_state(post, want, TOL64, name)
+    for k in ("sampling_dist", "eps_dist", "prev_pre_north", "prev_pre_east"):
+        assert rel_err(post[k], d["post_" + k], SCALE[k]).max() <= TOL64, k
+
+
+@pytest.mark.parametrize("name", ENV_CASES)
+def test_f64_free_running_vs_reference(name):
+    """Whole recorded episodes as fused multi-step launches with the recorded actions."""
+    d = golden(name)
+    T = len(d["reward"])
+    env = fixture_env(d, 1, 64)
+    assert np.array_equal(env.reset()[0].cpu().numpy(), d["reset_state"].astype(np.float64))
+    o = env_oracle(d)
+    env.set_state(env_state_from(d, "pre_", 0, o))
+    bounds = sorted({0, T, *[int(r) for r in d["resets"] if 0 < r < T]})
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        if a > 0:
+            env.reset()
+            env.init_step()
+        acts = {"action_ne": np.stack([d["action_n"][a:b], d["action_e"][a:b]], 1)[:, None, :],
+                "sac_update": d["sac_update"][a:b, None], "init": d["init"][a:b, None]}
+        out = env.rollout(b - a, actions=acts, auto_reset=False)
+        ns = out["next_state"][:, 0].cpu().numpy()
+        assert rel_err(ns, d["next_state"][a:b], OBS_SCALE).max() <= TOL64, f"{name} [{a},{b})"
+        assert rel_err(out["reward"][:, 0].cpu().numpy(), d["reward"][a:b], 1.0).max() <= TOL64
+        st = out["status"][:, 0].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        for i in range(b - a):
+            assert status_string(int(st[i])) == str(d["status"][a + i]), f"{name} step {a + i}"
+
+
+# ------------------------------------------------------------------------------------------
+# float64: synthetic-sampler rollouts against the oracle (C2 size), auto-reset included
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n_env,steps", [(4096, 300), (256, 2500)])
+def test_f64_synthetic_rollout_vs_oracle(n_env, steps):
+    sc = make_scenario(n_env, cap=32)
+    env = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+    env.reset()
+    env.init_step()
+    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+    o.reset()
+    o.init_step()
+    chunk = 100
+    for k0 in range(0, steps, chunk):
+        out = env.rollout(chunk, seed=25450)
+        r = o.rollout(chunk, seed=25450)
+        where = f"steps [{k0},{k0 + chunk})"
+        assert rel_err(out["next_state"].cpu().numpy(), r["next_state"], OBS_SCALE).max() <= TOL64, where
+        assert rel_err(out["reward"].cpu().numpy(), r["reward"], 1.0).max() <= TOL64, where
+        assert np.array_equal(out["done"].cpu().numpy().astype(bool), r["done"]), where
+        assert np.array_equal(out["status"].cpu().numpy().astype(np.int64) & 0xFFFFFFFF,
+                              r["status"].astype(np.int64)), where
+        act = out["action"].cpu().numpy()
+        assert np.array_equal(np.isnan(act[..., 2]), np.isnan(r["action"][..., 2])), where
+        assert rel_err(act[..., :2], r["action"][..., :2], 1e4).max() <= TOL64, where
+        assert np.array_equal(out["done_count"].cpu().numpy(), r["done"].sum(axis=1)), where
+    check_state(np_state(env), o.get_state(), 1e-8, "final state",
+                int_fields=so.SHIP_INT + ("ep_step", "event", "episodes"))
+
+
+# ------------------------------------------------------------------------------------------
+# float32: teacher-forced one step against the oracle
+# ------------------------------------------------------------------------------------------
+def test_f32_teacher_forced_vs_oracle():
+    n_env = 4096
+    sc = make_scenario(n_env, cap=32)
+    # realistic pre-states: a float64 rollout, snapshotted at several depths
+    env64 = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+    env64.reset()
+    env64.init_step()
+    env32 = VecMultiShipRLEnv(scenario=sc, precision=32, device=DEV)
+    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+    worst = {}
+    n_disc = 0
+    for depth in range(6):
+        env64.rollout(250, seed=11 + depth)
+        st = np_state(env64)
+        st32 = {k: (v.astype(np.float32).astype(np.float64) if v.dtype == np.float64 else v) for k, v in st.items()}
+        o.set_state(st32)
+        env32.set_state(st32)
+        rng = np.random.default_rng(depth)
+        sac = rng.random(n_env) < 0.1
+        ang = rng.uniform(-np.pi / 6, np.pi / 6, n_env)
+        act = np.stack([st32["north"][1] + o.ab_len * np.cos(o.ab_alpha + ang),
+                        st32["east"][1] + o.ab_len * np.sin(o.ab_alpha + ang)], 1)
+        act = act.astype(np.float32).astype(np.float64)
+        init = np.zeros(n_env, bool)
+        ns_r, rew_r, done_r, st_r = o.step(act, sac, init)
+        ns, rew, done, stat = env32.step(act, sac, init)
+        ns, rew, done, stat = ns.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy(), stat.cpu().numpy()
+        e = rel_err(ns, ns_r, OBS_SCALE)
+        worst["next_state"] = max(worst.get("next_state", 0), e.max())
+        # reward: terms up to 2000 plus O(1) shaping; tolerance 1e-5 * max(|r|, 1)
+        e = rel_err(rew, rew_r, 1.0)
+        ok = (done == done_r) & (stat == st_r)
+        worst["reward"] = max(worst.get("reward", 0), e[ok].max())
+        n_disc += int((~ok).sum())
+        post = np_state(env32)
+        ref = o.get_state()
+        for k in so.SHIP_REAL:
+            err = rel_err(post[k], ref[k], SCALE[k])[:, ok].max()
+            worst[k] = max(worst.get(k, 0), err)
+        for k in ("next_wpt", "n_wpt"):
+            assert np.array_equal(post[k], ref[k]), f"depth {depth}: {k}"
+    print("f32 teacher-forced worst:", {k: f"{v:.2e}" for k, v in worst.items()}, "discrete mismatches:", n_disc)
+    for k, v in worst.items():
+        assert v <= 1e-5, f"{k}: {v:.3e}"
+    assert n_disc <= 3, f"{n_disc} discrete mismatches (float32 knife edges)"
+
+
+# ------------------------------------------------------------------------------------------
+# API behaviour
+# ------------------------------------------------------------------------------------------
+def test_state_roundtrip_and_masks():
+    sc = make_scenario(300, cap=16)
+    env = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+    env.reset()
+    env.init_step()
+    env.rollout(50, seed=3)
+    blob = env.state_blob()
+    out1 = env.rollout(20, seed=4)
+    env.load_state_blob(blob)
+    out2 = env.rollout(20, seed=4)
+    assert torch.equal(out1["next_state"], out2["next_state"])
+    # masked reset touches only masked envs; shaft speed and integrators persist (Q6)
+    before = np_state(env)
+    mask = np.zeros(300, bool)
+    mask[::3] = True
+    init_obs = env.reset(mask).cpu().numpy()
+    after = np_state(env)
+    assert np.array_equal(after["north"][:, ~mask], before["north"][:, ~mask])
+    assert np.allclose(after["north"][:, mask], sc.init[mask, :, 0].T)
+    for k in ("shaft_speed", "ship_speed_i", "shaft_speed_i", "heading_i", "heading_prev"):
+        assert np.array_equal(after[k], before[k]), k
+    assert np.all(after["next_wpt"][:, mask] == 1) and np.all(after["e_ct_int"][:, mask] == 0)
+    assert np.allclose(init_obs[:, 0], sc.init[:, 0, 0].astype(np.float32))
+
+
+def test_route_overflow_flag():
+    """Insertions beyond the route capacity are dropped and flagged (SIT_ST_ROUTE_OVERFLOW)."""
+    sc = make_scenario(64, cap=4)
+    env = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+    env.reset()
+    env.init_step()
+    st = np_state(env)
+    act = np.stack([st["north"][1] + 500.0, st["east"][1]], 1)
+    flags = []
+    for i in range(4):
+        _, _, _, status = env.step(act, np.ones(64, bool), np.full(64, i == 0))
+        flags.append(status.cpu().numpy())
+    nw = np_state(env)["n_wpt"][1]
+    assert np.all(nw == 4)
+    assert not (flags[0] & (1 << 31)).any() and not (flags[1] & (1 << 31)).any()
+    assert (flags[2] & (1 << 31)).all() and (flags[3] & (1 << 31)).all()
+
+
+def test_done_count_and_large_batch_sanity():
+    """C3 size: 65 536 ships (32 768 envs) fused rollout; finite outputs, done_count = sum(done)."""
+    env = VecMultiShipRLEnv(n_env=32768, precision=32, device=DEV)
+    env.reset()
+    env.init_step()
+    out = env.rollout(500, seed=1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out["next_state"]).all()
+    assert torch.isfinite(out["reward"]).all()
+    assert torch.equal(out["done_count"].to(torch.int64), out["done"].to(torch.int64).sum(1))
