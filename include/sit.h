@@ -213,7 +213,7 @@ int sit_restart(sit_handle* h, void* stream);
 /* ---- stepping (device pointers, stream-ordered) ------------------------------------ */
 /* MultiShipRLEnv.reset for envs with env_mask[e] != 0 (NULL = all).  Keeps shaft speed and
  * all PI/PID integrator states, as the reference does.  If initial_state is not NULL it
- * receives the construction-time observation, real[n_env][SIT_OBS_DIM]. */
+ * receives the construction-time observation of every env, real[n_env][SIT_OBS_DIM]. */
 int sit_reset(sit_handle* h, const uint8_t* env_mask, void* initial_state, void* stream);
 /* MultiShipRLEnv.init_step for masked envs (NULL = all). */
 int sit_init_step(sit_handle* h, const uint8_t* env_mask, void* stream);

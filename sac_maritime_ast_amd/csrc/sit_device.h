@@ -72,16 +72,19 @@ struct Consts {
   T pi6;
 };
 
-// island map: polygon p owns edges [off[p], off[p+1]); edge i goes from vertex i to vertex
-// nxt[i] (ring closed).  Vertex coordinates are (x = east, y = north) as in obstacle.py:128.
+// island map: polygon p owns edges [off[p], off[p+1]); edge i runs from (ax, ay) to (bx, by)
+// (ring closed).  Coordinates are (x = east, y = north) as in obstacle.py:128.  The step kernel
+// stages these arrays in LDS once per launch; every lane then reads them as broadcasts.
 template <typename T>
 struct Map {
   int32_t n_poly;
+  int32_t n_edge;
   const int32_t* off;   // [n_poly + 1]
-  const T* vx;          // [n_vert] east
-  const T* vy;          // [n_vert] north
-  const int32_t* nxt;   // [n_vert] index of the next ring vertex
-  const T* inv_len2;    // [n_vert] 1 / |edge|^2 (0 for a degenerate edge)
+  const T* ax;          // [n_edge]
+  const T* ay;
+  const T* bx;
+  const T* by;
+  const T* inv_len2;    // [n_edge] 1 / |edge|^2 (0 for a degenerate edge)
   const T* bbox;        // [n_poly][4] min_x, max_x, min_y, max_y
 };
 
@@ -289,9 +292,8 @@ __device__ bool point_in_polys(const Map<T>& m, T n, T e) {
     int cross = 0;
     bool onb = false;
     for (int i = m.off[p]; i < m.off[p + 1]; ++i) {
-      const T p1x = m.vx[i], p1y = m.vy[i];
-      const int j = m.nxt[i];
-      const T p2x = m.vx[j], p2y = m.vy[j];
+      const T p1x = m.ax[i], p1y = m.ay[i];
+      const T p2x = m.bx[i], p2y = m.by[i];
       if (p1x < qx && p2x < qx) continue;
       if (qx == p2x && qy == p2y) { onb = true; break; }
       if (p1y == qy && p2y == qy) {
@@ -316,11 +318,9 @@ template <typename T>
 __device__ T distance_to_polys(const Map<T>& m, T n, T e) {
   const T px = e, py = n;
   T best = T(3.0e38);
-  const int nv = m.off[m.n_poly];
-  for (int i = 0; i < nv; ++i) {
-    const T ax = m.vx[i], ay = m.vy[i];
-    const int j = m.nxt[i];
-    const T bx = m.vx[j], by = m.vy[j];
+  for (int i = 0; i < m.n_edge; ++i) {
+    const T ax = m.ax[i], ay = m.ay[i];
+    const T bx = m.bx[i], by = m.by[i];
     const T ex = bx - ax, ey = by - ay;
     const T qx = px - ax, qy = py - ay;
     const T t = qx * ex + qy * ey;

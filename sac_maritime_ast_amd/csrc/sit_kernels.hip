@@ -112,13 +112,35 @@ struct StepIO {
 template <typename T>
 struct KArgs {
   Consts<T> c;
-  Map<T> map;
+  Map<T> map;       // global copy (base pointer = map.off, size map_bytes)
   State<T> st;
   Scen<T> sc;
   StepIO<T> io;
   int32_t n_env;
   int32_t cap;
+  int32_t map_bytes;
 };
+
+// Copy the map blob (offsets, edge arrays, bboxes: one contiguous allocation) into LDS at
+// `dst` and return a Map whose pointers address the LDS copy.
+template <typename T>
+__device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* dst) {
+  const unsigned char* src = reinterpret_cast<const unsigned char*>(a.map.off);
+  const int n16 = a.map_bytes / 16;
+  for (int i = threadIdx.x; i < n16; i += blockDim.x)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  auto rebase = [&](const auto* p) {
+    using P = std::remove_cv_t<std::remove_pointer_t<decltype(p)>>;
+    return reinterpret_cast<const P*>(dst + (reinterpret_cast<const unsigned char*>(p) - src));
+  };
+  Map<T> m = a.map;
+  m.off = rebase(a.map.off);
+  m.ax = rebase(a.map.ax); m.ay = rebase(a.map.ay);
+  m.bx = rebase(a.map.bx); m.by = rebase(a.map.by);
+  m.inv_len2 = rebase(a.map.inv_len2);
+  m.bbox = rebase(a.map.bbox);
+  return m;
+}
 
 }  // namespace
 
@@ -212,6 +234,9 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Xchg<T> xs[2];
   const Consts<T>& c = a.c;
+  // LDS: [map blob][route tables if STAGE]
+  const Map<T> map = stage_map(a, smem);
+  unsigned char* route_lds = smem + ((a.map_bytes + 255) & ~255);
   const int lane = threadIdx.x & (kWave - 1);
   const int type = threadIdx.x >> 6;             // wave-uniform
   const int n_env = a.n_env;
@@ -235,7 +260,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     T* gn = a.st.wn + (size_t)type * a.cap * n_env + env;
     T* ge = a.st.we + (size_t)type * a.cap * n_env + env;
     if (STAGE) {
-      T* ln = reinterpret_cast<T*>(smem) + (size_t)type * a.cap * kWave + lane;
+      T* ln = reinterpret_cast<T*>(route_lds) + (size_t)type * a.cap * kWave + lane;
       T* le = ln + (size_t)2 * a.cap * kWave;
       for (int i = 0; i < rt.nw - 1; ++i) {
         ln[i * kWave] = gn[(size_t)i * n_env];
@@ -257,6 +282,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     }
   }
   const T maxn = c.max_n;
+  __syncthreads();   // map staged
 
   for (int step = 0; step < a.io.n_steps; ++step) {
     const size_t row = (size_t)step * n_env + env;
@@ -334,11 +360,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       }
 
       // ---------------- own termination predicates (MSRL_env_ex.py:628-881) ----------------
-      const T dobst = distance_to_polys(a.map, s.n, s.e);
+      const T dobst = distance_to_polys(map, s.n, s.e);
       const T dn_end = s.n - rt.end_n, de_end = s.e - rt.end_e;
       const bool arrive = xsqrt(dn_end * dn_end + de_end * de_end) <= c.arrival_radius;
       const bool horizon = outside(c, s.n, s.e, c.half_len);
-      const bool terrain = hull_in_terrain(c, a.map, s.n, s.e);
+      const bool terrain = hull_in_terrain(c, map, s.n, s.e);
       int stop = s.stop;
       bool done = false;
       if (type == 0) {
@@ -366,7 +392,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           done = true;
           bits |= SIT_ST_OBS_TERRAIN;
         }
-        if (outside(c, iwn, iwe, T(0)) || point_in_polys(a.map, iwn, iwe)) {   // Q11
+        if (outside(c, iwn, iwe, T(0)) || point_in_polys(map, iwn, iwe)) {   // Q11
           if (!stop) r_term = r_term - T(1000);
           stop = 1; done = true;
           bits |= SIT_ST_OBS_IW_TERMINAL;
@@ -495,9 +521,11 @@ __global__ __launch_bounds__(256) void k_reset(const KArgs<T> a, const uint8_t* 
     a.st.env[0][env] = T(0);
     a.st.env[1][env] = T(0);
     a.st.ep_step[env] = 0;
-    if (initial_state)
-      for (int j = 0; j < SIT_OBS_DIM; ++j) initial_state[(size_t)env * SIT_OBS_DIM + j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
   }
+  // the construction-time observation (constant per env) is returned for every env
+  if (initial_state)
+    for (int j = 0; j < SIT_OBS_DIM; ++j)
+      initial_state[(size_t)env * SIT_OBS_DIM + j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
 }
 
 // construction-time state (one thread per env)
@@ -546,7 +574,8 @@ struct sit_handle {
   // map
   unsigned char* map = nullptr;
   int n_poly = 0, n_vert = 0;
-  size_t map_off = 0, map_vx = 0, map_vy = 0, map_nxt = 0, map_il2 = 0, map_bbox = 0;
+  size_t map_off = 0, map_ax = 0, map_ay = 0, map_bx = 0, map_by = 0, map_il2 = 0, map_bbox = 0;
+  size_t map_bytes = 0;
   double min_n = 0, max_n = 0, min_e = 0, max_e = 0;
   bool have_map = false, have_routes = false, have_init = false;
 };
@@ -680,12 +709,15 @@ KArgs<T> make_args(const sit_handle* h) {
   a.sc.ab_alpha = reinterpret_cast<const double*>(h->scen + h->scen_ab_alpha);
   a.sc.initial_state = reinterpret_cast<const T*>(h->scen + h->scen_initial);
   a.map.n_poly = h->n_poly;
+  a.map.n_edge = h->n_vert;
   a.map.off = reinterpret_cast<const int32_t*>(h->map + h->map_off);
-  a.map.vx = reinterpret_cast<const T*>(h->map + h->map_vx);
-  a.map.vy = reinterpret_cast<const T*>(h->map + h->map_vy);
-  a.map.nxt = reinterpret_cast<const int32_t*>(h->map + h->map_nxt);
+  a.map.ax = reinterpret_cast<const T*>(h->map + h->map_ax);
+  a.map.ay = reinterpret_cast<const T*>(h->map + h->map_ay);
+  a.map.bx = reinterpret_cast<const T*>(h->map + h->map_bx);
+  a.map.by = reinterpret_cast<const T*>(h->map + h->map_by);
   a.map.inv_len2 = reinterpret_cast<const T*>(h->map + h->map_il2);
   a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
+  a.map_bytes = (int32_t)h->map_bytes;
   return a;
 }
 
@@ -698,7 +730,8 @@ int ready(sit_handle* h) {
 }
 
 template <typename T>
-size_t stage_lds_bytes(const sit_handle* h) { return (size_t)2 * 2 * h->cap * kWave * sizeof(T); }
+size_t route_lds_bytes(const sit_handle* h) { return (size_t)2 * 2 * h->cap * kWave * sizeof(T); }
+size_t map_lds_bytes(const sit_handle* h) { return (h->map_bytes + 255) & ~size_t(255); }
 
 template <typename T>
 int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
@@ -706,24 +739,22 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   a.io = io;
   const int blocks = (h->n_env + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const bool synth = io.action_ne == nullptr;
-  const size_t lds = stage_lds_bytes<T>(h);
-  const bool stage = io.n_steps > 1 && lds <= 96 * 1024;
-  if (stage) {
-    if (synth)
-      HIP_TRY(h, hipFuncSetAttribute((const void*)k_env_steps<T, true, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    else
-      HIP_TRY(h, hipFuncSetAttribute((const void*)k_env_steps<T, false, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const size_t rlds = route_lds_bytes<T>(h);
+  const bool stage = io.n_steps > 1 && rlds + map_lds_bytes(h) <= 112 * 1024;
+  const size_t lds = map_lds_bytes(h) + (stage ? rlds : 0);
+  {
+    const void* fn = synth ? (stage ? (const void*)k_env_steps<T, true, true> : (const void*)k_env_steps<T, true, false>)
+                           : (stage ? (const void*)k_env_steps<T, false, true> : (const void*)k_env_steps<T, false, false>);
+    HIP_TRY(h, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   }
   if (synth && stage)
     hipLaunchKernelGGL((k_env_steps<T, true, true>), dim3(blocks), dim3(128), lds, stream, a);
   else if (synth)
-    hipLaunchKernelGGL((k_env_steps<T, true, false>), dim3(blocks), dim3(128), 0, stream, a);
+    hipLaunchKernelGGL((k_env_steps<T, true, false>), dim3(blocks), dim3(128), lds, stream, a);
   else if (stage)
     hipLaunchKernelGGL((k_env_steps<T, false, true>), dim3(blocks), dim3(128), lds, stream, a);
   else
-    hipLaunchKernelGGL((k_env_steps<T, false, false>), dim3(blocks), dim3(128), 0, stream, a);
+    hipLaunchKernelGGL((k_env_steps<T, false, false>), dim3(blocks), dim3(128), lds, stream, a);
   HIP_TRY(h, hipGetLastError());
   return SIT_OK;
 }
@@ -888,31 +919,36 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     h->min_e = std::min(h->min_e, bx0); h->max_e = std::max(h->max_e, bx1);
     h->min_n = std::min(h->min_n, by0); h->max_n = std::max(h->max_n, by1);
   }
+  std::vector<double> bxv(nv), byv(nv);
   for (int i = 0; i < nv; ++i) {
-    const double ex = vx[nxt[i]] - vx[i], ey = vy[nxt[i]] - vy[i];
+    bxv[i] = vx[nxt[i]];
+    byv[i] = vy[nxt[i]];
+    const double ex = bxv[i] - vx[i], ey = byv[i] - vy[i];
     const double l2 = ex * ex + ey * ey;
     il2[i] = l2 > 0 ? 1.0 / l2 : 0.0;
   }
   size_t o = 0;
   h->map_off = o; o = align256(o + (n_poly + 1) * 4);
-  h->map_vx = o; o = align256(o + nv * rs);
-  h->map_vy = o; o = align256(o + nv * rs);
-  h->map_nxt = o; o = align256(o + nv * 4);
+  h->map_ax = o; o = align256(o + nv * rs);
+  h->map_ay = o; o = align256(o + nv * rs);
+  h->map_bx = o; o = align256(o + nv * rs);
+  h->map_by = o; o = align256(o + nv * rs);
   h->map_il2 = o; o = align256(o + nv * rs);
   h->map_bbox = o; o = align256(o + 4 * n_poly * rs);
   std::vector<unsigned char> host(o, 0);
   std::memcpy(host.data() + h->map_off, offs.data(), (n_poly + 1) * 4);
-  std::memcpy(host.data() + h->map_nxt, nxt.data(), nv * 4);
   auto put = [&](size_t at, const std::vector<double>& src) {
     for (size_t i = 0; i < src.size(); ++i) {
       if (rs == 8) reinterpret_cast<double*>(host.data() + at)[i] = src[i];
       else reinterpret_cast<float*>(host.data() + at)[i] = (float)src[i];
     }
   };
-  put(h->map_vx, vx); put(h->map_vy, vy); put(h->map_il2, il2); put(h->map_bbox, bbox);
+  put(h->map_ax, vx); put(h->map_ay, vy); put(h->map_bx, bxv); put(h->map_by, byv);
+  put(h->map_il2, il2); put(h->map_bbox, bbox);
   if (h->map) { (void)hipFree(h->map); h->map = nullptr; }
   HIP_TRY(h, hipMalloc(&h->map, o));
   HIP_TRY(h, hipMemcpy(h->map, host.data(), o, hipMemcpyHostToDevice));
+  h->map_bytes = o;
   h->n_poly = n_poly;
   h->n_vert = nv;
   h->have_map = true;
