@@ -82,6 +82,11 @@ extern "C" {
 
 /* ---- next_state layout (MSRL_Env.py:426-437) --------------------------------------- */
 #define SIT_OBS_DIM 10 /* test n,e,psi,rpm,|e_ct|,P_me[kW], obs n,e,psi,|e_ct| */
+/* ---- replay transition record (memory.push, test_beds/main_ast.py:385-396) ----------
+ *   [0:10] state (the observation before the step; reset()'s array at an episode start)
+ *   [10] action (scoping angle a), [11] reward, [12:22] next_state,
+ *   [22] mask (1 if the episode step reaches mask_horizon, else not done), [23] env id */
+#define SIT_TRANSITION_DIM 24
 
 /* ---- per-ship initial values for sit_load_initial ---------------------------------- */
 enum {
@@ -252,6 +257,13 @@ typedef struct sit_rollout_args {
   uint32_t* status;          /* u32[n_steps][n_env] or NULL */
   void* action_out;          /* real[n_steps][n_env][4] or NULL */
   int32_t* done_count;       /* int32[n_steps] or NULL: += envs done at each step */
+  /* sampling-event transitions (synthetic sampler mode): one record per step whose
+   * SAC_update is set, appended at transition_count (atomic); records beyond
+   * transition_capacity are counted but not written */
+  void* transitions;          /* real[transition_capacity][SIT_TRANSITION_DIM] or NULL */
+  int32_t* transition_count;  /* int32[1] */
+  int32_t transition_capacity;
+  int32_t mask_horizon;       /* args.num_steps_episode (main_ast.py:71, 387); 0 = none */
 } sit_rollout_args;
 int sit_rollout(sit_handle* h, const sit_rollout_args* a, void* stream);
 

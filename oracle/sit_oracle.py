@@ -347,6 +347,7 @@ class OracleEnvs:
             s[name] = np.zeros(n)
         for name in ENV_INT:
             s[name] = np.zeros(n, dtype=np.int64)
+        s["last_obs"] = self.initial_state.T.astype(np.float64).copy()   # sampler's `state`
         self.s = s
 
     def get_state(self):
@@ -536,6 +537,7 @@ class OracleEnvs:
         for name in ("sampling_dist", "eps_dist"):
             s[name][m] = 0.0
         s["ep_step"][m] = 0
+        s["last_obs"][:, m] = self.initial_state[m].T
         return self.initial_state.copy()
 
     def init_step(self, mask=None):
@@ -610,6 +612,7 @@ class OracleEnvs:
         reward, done, st = self._reward(ns, action_ne)
         status |= st
         s["ep_step"] += 1
+        s["last_obs"] = ns.T.copy()
         return ns, reward, done, status
 
     # ---------------- reward_function (MSRL_env_ex.py:906-980) ----------------
@@ -719,17 +722,28 @@ class OracleEnvs:
         act = np.stack([s["iw_north"], s["iw_east"]], axis=1)
         return act, sample, init, np.where(sample, a, np.nan)
 
-    def rollout(self, n_steps, seed, auto_reset=True, env_id_offset=0, actions=None):
+    def rollout(self, n_steps, seed, auto_reset=True, env_id_offset=0, actions=None, mask_horizon=600):
         """K steps of the test_beds/main_ast.py:310-412 loop: reset+init_step on done, synthetic
-        (or explicit) IW actions.  Returns dict of [K, n_env, ...] arrays."""
+        (or explicit) IW actions.  Returns dict of [K, n_env, ...] arrays plus the replay
+        transitions pushed on sampling events (main_ast.py:385-396) as rows of
+        [state 10, a, reward, next_state 10, mask, env id]."""
         out = dict(next_state=[], reward=[], done=[], status=[], action=[])
+        trans = []
         for k in range(n_steps):
             if actions is None:
                 act, sac, init, ang = self.sampler_actions(seed, env_id_offset)
             else:
                 act, sac, init = actions["action_ne"][k], actions["sac_update"][k], actions["init"][k]
                 ang = np.full(self.n_env, np.nan)
+            state = self.s["last_obs"].T.copy()
+            t_after = self.s["ep_step"] + 1
             ns, rew, done, st = self.step(act, sac, init)
+            if actions is None and np.any(sac):
+                idx = np.nonzero(sac)[0]
+                mask = np.where((mask_horizon > 0) & (t_after + 1 == mask_horizon), 1.0, 1.0 - done)
+                rec = np.concatenate([state[idx], ang[idx, None], rew[idx, None], ns[idx], mask[idx, None],
+                                      (idx + env_id_offset)[:, None].astype(np.float64)], axis=1)
+                trans.append(rec)
             out["next_state"].append(ns)
             out["reward"].append(rew)
             out["done"].append(done)
@@ -739,7 +753,9 @@ class OracleEnvs:
                 self.reset(done)
                 self.s["episodes"] = self.s["episodes"] + done.astype(np.int64)
                 self.init_step(done)
-        return {k: np.stack(v) for k, v in out.items()}
+        res = {k: np.stack(v) for k, v in out.items()}
+        res["transitions"] = np.concatenate(trans) if trans else np.zeros((0, 24))
+        return res
 
 
 def status_string(bits: int) -> str:

@@ -17,6 +17,7 @@ SIT_F32, SIT_F64 = 32, 64
 SIT_SG_MOTOR, SIT_SG_GEN, SIT_SG_OFF = 0, 1, 2
 SIT_DT_REAL, SIT_DT_I32, SIT_DT_U32 = 0, 1, 2
 SIT_OBS_DIM = 10
+SIT_TRANSITION_DIM = 24
 INIT_FIELDS = ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed", "desired_speed",
                "ship_speed_i", "shaft_speed_i")
 
@@ -70,6 +71,8 @@ class RolloutArgs(ctypes.Structure):
         ("action_ne", c_void_p), ("sac_update", c_void_p), ("init", c_void_p),
         ("next_state", c_void_p), ("reward", c_void_p), ("done", c_void_p), ("status", c_void_p),
         ("action_out", c_void_p), ("done_count", c_void_p),
+        ("transitions", c_void_p), ("transition_count", c_void_p), ("transition_capacity", c_int32),
+        ("mask_horizon", c_int32),
     ]
 
 

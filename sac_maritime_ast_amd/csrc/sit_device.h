@@ -75,10 +75,22 @@ struct Consts {
 // island map: polygon p owns edges [off[p], off[p+1]); edge i runs from (ax, ay) to (bx, by)
 // (ring closed).  Coordinates are (x = east, y = north) as in obstacle.py:128.  The step kernel
 // stages these arrays in LDS once per launch; every lane then reads them as broadcasts.
+//
+// Spatial index (built on the host by sit_load_map, exact by construction):
+//  * grid: G x G cells over the map extent plus a margin; cell c lists every edge that can be
+//    the nearest edge of some point within 1 m of the cell (conservative bound with a 1 m
+//    float slack), so the minimum over the list equals the minimum over all edges.
+//  * bands: NB horizontal bands; band b lists every edge whose y-range meets the band (+-1 m).
+//    The ray-crossing test of GEOS only ever looks at edges whose y-range contains the
+//    point's y, so scanning the band's list gives the same crossings.
+constexpr int kGrid = 32;
+constexpr int kBands = 64;
+
 template <typename T>
 struct Map {
   int32_t n_poly;
   int32_t n_edge;
+  int32_t use_index;    // 0: full scans only
   const int32_t* off;   // [n_poly + 1]
   const T* ax;          // [n_edge]
   const T* ay;
@@ -86,6 +98,13 @@ struct Map {
   const T* by;
   const T* inv_len2;    // [n_edge] 1 / |edge|^2 (0 for a degenerate edge)
   const T* bbox;        // [n_poly][4] min_x, max_x, min_y, max_y
+  const uint8_t* poly;  // [n_edge] polygon of the edge
+  const uint16_t* grid_start;  // [kGrid * kGrid + 1]
+  const uint8_t* grid_idx;
+  const uint16_t* band_start;  // [kBands + 1]
+  const uint8_t* band_idx;
+  T gx0, gy0, ginvx, ginvy;    // grid origin and 1 / cell size
+  T by0, binv;                 // band origin and 1 / band height
 };
 
 // --------------------------------------------------------------------------------------
@@ -338,6 +357,89 @@ __device__ T distance_to_polys(const Map<T>& m, T n, T e) {
     best = xmin(best, d2);
   }
   return xsqrt(best);
+}
+
+// squared distance from p to edge i (GEOS Distance::pointToSegment, squared form)
+template <typename T>
+__device__ __forceinline__ T edge_dist2(const Map<T>& m, int i, T px, T py) {
+  const T ax = m.ax[i], ay = m.ay[i];
+  const T ex = m.bx[i] - ax, ey = m.by[i] - ay;
+  const T qx = px - ax, qy = py - ay;
+  const T t = qx * ex + qy * ey;
+  const T il2 = m.inv_len2[i];
+  if (il2 == T(0) || t <= T(0)) return qx * qx + qy * qy;
+  if (t * il2 >= T(1)) {
+    const T rx = px - m.bx[i], ry = py - m.by[i];
+    return rx * rx + ry * ry;
+  }
+  const T cr = qy * ex - qx * ey;
+  return cr * cr * il2;
+}
+
+// distance to the nearest polygon boundary via the grid's candidate lists (same value as
+// distance_to_polys: the lists contain every possible minimiser)
+template <typename T>
+__device__ T distance_indexed(const Map<T>& m, T n, T e) {
+  const T fx = (e - m.gx0) * m.ginvx, fy = (n - m.gy0) * m.ginvy;
+  if (!m.use_index || !(fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)))
+    return distance_to_polys(m, n, e);
+  const int c = (int)fy * kGrid + (int)fx;
+  T best = T(3.0e38);
+  const int k1 = m.grid_start[c + 1];
+  for (int k = m.grid_start[c]; k < k1; ++k) best = xmin(best, edge_dist2(m, m.grid_idx[k], e, n));
+  return xsqrt(best);
+}
+
+// GEOS RayCrossingCounter::countSegment for one segment, per polygon bitmasks
+template <typename T>
+__device__ __forceinline__ void count_segment(T p1x, T p1y, T p2x, T p2y, T qx, T qy, uint32_t bit,
+                                              uint32_t& parity, uint32_t& onb) {
+  if (p1x < qx && p2x < qx) return;
+  if (qx == p2x && qy == p2y) { onb |= bit; return; }
+  if (p1y == qy && p2y == qy) {
+    if (xmin(p1x, p2x) <= qx && qx <= xmax(p1x, p2x)) onb |= bit;
+    return;
+  }
+  if ((p1y > qy && p2y <= qy) || (p2y > qy && p1y <= qy)) {
+    int o = orientation(p1x, p1y, p2x, p2y, qx, qy);
+    if (o == 0) { onb |= bit; return; }
+    if (p2y < p1y) o = -o;
+    if (o > 0) parity ^= bit;
+  }
+}
+
+// Polygon.contains for two points sharing y (= n): returns bit 0 / bit 1 for x0 / x1
+template <typename T>
+__device__ int pip_pair_indexed(const Map<T>& m, T n, T x0, T x1) {
+  if (!m.use_index) return (int)point_in_polys(m, n, x0) | ((int)point_in_polys(m, n, x1) << 1);
+  const T fb = (n - m.by0) * m.binv;
+  if (!(fb >= T(0) && fb < T(kBands))) return 0;   // beyond every edge's y-range
+  const int b = (int)fb;
+  uint32_t par0 = 0, onb0 = 0, par1 = 0, onb1 = 0;
+  const int k1 = m.band_start[b + 1];
+  for (int k = m.band_start[b]; k < k1; ++k) {
+    const int i = m.band_idx[k];
+    const T p1x = m.ax[i], p1y = m.ay[i], p2x = m.bx[i], p2y = m.by[i];
+    const uint32_t bit = 1u << m.poly[i];
+    count_segment(p1x, p1y, p2x, p2y, x0, n, bit, par0, onb0);
+    count_segment(p1x, p1y, p2x, p2y, x1, n, bit, par1, onb1);
+  }
+  return ((par0 & ~onb0) != 0 ? 1 : 0) | ((par1 & ~onb1) != 0 ? 2 : 0);
+}
+
+template <typename T>
+__device__ bool pip_indexed(const Map<T>& m, T n, T e) {
+  if (!m.use_index) return point_in_polys(m, n, e);
+  const T fb = (n - m.by0) * m.binv;
+  if (!(fb >= T(0) && fb < T(kBands))) return false;
+  const int b = (int)fb;
+  uint32_t par = 0, onb = 0;
+  const int k1 = m.band_start[b + 1];
+  for (int k = m.band_start[b]; k < k1; ++k) {
+    const int i = m.band_idx[k];
+    count_segment(m.ax[i], m.ay[i], m.bx[i], m.by[i], e, n, 1u << m.poly[i], par, onb);
+  }
+  return (par & ~onb) != 0;
 }
 
 }  // namespace sit

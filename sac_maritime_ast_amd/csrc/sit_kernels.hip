@@ -32,7 +32,7 @@ using namespace sit;
 // ---------------------------------------------------------------------------------------
 namespace {
 
-enum Extent { kShip = 0, kEnv = 1, kTable = 2 };
+enum Extent { kShip = 0, kEnv = 1, kTable = 2, kObs = 3 };
 struct FieldSpec {
   const char* name;
   int dtype;
@@ -58,11 +58,12 @@ const FieldSpec kFields[] = {
     {"ep_step", SIT_DT_I32, kEnv},        {"event", SIT_DT_U32, kEnv},
     {"episodes", SIT_DT_U32, kEnv},
     {"wpt_north", SIT_DT_REAL, kTable},   {"wpt_east", SIT_DT_REAL, kTable},
+    {"last_obs", SIT_DT_REAL, kObs},
 };
 constexpr int kNumFields = (int)(sizeof(kFields) / sizeof(kFields[0]));
 enum FieldId {
   F_NORTH = 0, F_LAST_PME = 14, F_K = 15, F_NW, F_TICKS, F_STOP,
-  F_SAMP = 19, F_IW_E = 24, F_EP = 25, F_EVENT, F_EPISODES, F_WN, F_WE
+  F_SAMP = 19, F_IW_E = 24, F_EP = 25, F_EVENT, F_EPISODES, F_WN, F_WE, F_LAST_OBS
 };
 
 // per-env scenario (constant after sit_load_*), device side
@@ -90,6 +91,7 @@ struct State {
   uint32_t* episodes;
   T* wn;                  // [2][cap][n_env]
   T* we;
+  T* last_obs;            // [SIT_OBS_DIM][n_env]: observation before the next step
 };
 
 template <typename T>
@@ -107,6 +109,10 @@ struct StepIO {
   uint32_t* status;
   T* action_out;
   int32_t* done_count;
+  T* transitions;
+  int32_t* transition_count;
+  int32_t transition_capacity;
+  int32_t mask_horizon;
 };
 
 template <typename T>
@@ -139,6 +145,11 @@ __device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* ds
   m.bx = rebase(a.map.bx); m.by = rebase(a.map.by);
   m.inv_len2 = rebase(a.map.inv_len2);
   m.bbox = rebase(a.map.bbox);
+  m.poly = rebase(a.map.poly);
+  m.grid_start = rebase(a.map.grid_start);
+  m.grid_idx = rebase(a.map.grid_idx);
+  m.band_start = rebase(a.map.band_start);
+  m.band_idx = rebase(a.map.band_idx);
   return m;
 }
 
@@ -204,12 +215,12 @@ __device__ __forceinline__ bool outside(const Consts<T>& c, T n, T e, T margin) 
   return n < c.min_n + margin || n > c.max_n - margin || e < c.min_e + margin || e > c.max_e - margin;
 }
 
-// is_pos_inside_obstacles: 4 corners of a +-l/2 square (MSRL_env_ex.py:490-515)
+// is_pos_inside_obstacles: 4 corners of a +-l/2 square (MSRL_env_ex.py:490-515); the two
+// corners of one side share a y and one band scan
 template <typename T>
 __device__ __forceinline__ bool hull_in_terrain(const Consts<T>& c, const Map<T>& m, T n, T e) {
   const T h = c.half_len;
-  return point_in_polys(m, n - h, e - h) | point_in_polys(m, n - h, e + h) |
-         point_in_polys(m, n + h, e - h) | point_in_polys(m, n + h, e + h);
+  return (pip_pair_indexed(m, n - h, e - h, e + h) | pip_pair_indexed(m, n + h, e - h, e + h)) != 0;
 }
 
 constexpr uint32_t kStopBit = 1u << 30;   // exchange-only: stop flag after this ship's checks
@@ -222,6 +233,7 @@ struct Xchg {
   T r_nto[kWave];
   T r_o[kWave];
   uint32_t bits[2][kWave];
+  int32_t slot[kWave];    // transition record of this step (obstacle lane allocates)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -251,7 +263,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   int ep_step = 0;
   uint32_t event = 0, episodes = 0;
   double ab_len = 0.0, ab_alpha = 0.0;
+  T lo[6] = {};                      // this ship's part of the last observation
+  const int lo_base = type == 0 ? 0 : 6, lo_n = type == 0 ? 6 : 4;
   if (act) {
+    for (int j = 0; j < lo_n; ++j) lo[j] = a.st.last_obs[(size_t)(lo_base + j) * n_env + env];
+    ep_step = a.st.ep_step[env];
     load_ship(a.st, sid, s);
     rt.nw = a.st.nw[sid];
     rt.end_n = a.sc.end_n[sid];
@@ -274,7 +290,6 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       samp = a.st.env[0][env]; eps = a.st.env[1][env];
       ppn = a.st.env[2][env]; ppe = a.st.env[3][env];
       iwn = a.st.env[4][env]; iwe = a.st.env[5][env];
-      ep_step = a.st.ep_step[env];
       event = a.st.event[env];
       episodes = a.st.episodes[env];
       ab_len = a.sc.ab_len[env];
@@ -360,7 +375,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       }
 
       // ---------------- own termination predicates (MSRL_env_ex.py:628-881) ----------------
-      const T dobst = distance_to_polys(map, s.n, s.e);
+      const T dobst = distance_indexed(map, s.n, s.e);
       const T dn_end = s.n - rt.end_n, de_end = s.e - rt.end_e;
       const bool arrive = xsqrt(dn_end * dn_end + de_end * de_end) <= c.arrival_radius;
       const bool horizon = outside(c, s.n, s.e, c.half_len);
@@ -392,7 +407,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           done = true;
           bits |= SIT_ST_OBS_TERRAIN;
         }
-        if (outside(c, iwn, iwe, T(0)) || point_in_polys(map, iwn, iwe)) {   // Q11
+        if (outside(c, iwn, iwe, T(0)) || pip_indexed(map, iwn, iwe)) {   // Q11
           if (!stop) r_term = r_term - T(1000);
           stop = 1; done = true;
           bits |= SIT_ST_OBS_IW_TERMINAL;
@@ -405,6 +420,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         if (done) bits |= SIT_ST_OBS_DONE;
       }
       s.stop = stop;
+      if (type == 1) {
+        int slot = -1;
+        if (a.io.transitions && sac) slot = atomicAdd(a.io.transition_count, 1);
+        x.slot[lane] = slot;
+      }
       x.n[type][lane] = s.n;
       x.e[type][lane] = s.e;
       x.bits[type][lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u);
@@ -426,6 +446,15 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
         if (a.io.reward) a.io.reward[row] = reward;
         if (a.io.done) a.io.done[row] = env_done ? 1 : 0;
+        const int slot = x.slot[lane];
+        if (slot >= 0 && slot < a.io.transition_capacity) {
+          T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
+          for (int j = 0; j < 6; ++j) rec[j] = lo[j];
+          rec[11] = reward;
+          rec[12] = s.n; rec[13] = s.e; rec[14] = s.psi; rec[15] = o_rpm; rec[16] = o_ect; rec[17] = o_pme;
+          const bool horizon_hit = a.io.mask_horizon > 0 && ep_step + 2 == a.io.mask_horizon;
+          rec[22] = (horizon_hit || !env_done) ? T(1) : T(0);
+        }
         if (a.io.status) a.io.status[row] = status;
         if (a.io.next_state) {
           T* ns = a.io.next_state + row * SIT_OBS_DIM;
@@ -440,7 +469,18 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           T* ao = a.io.action_out + row * 4;
           ao[0] = iwn; ao[1] = iwe; ao[2] = (T)ang; ao[3] = sac ? T(1) : T(0);
         }
+        const int slot = x.slot[lane];
+        if (slot >= 0 && slot < a.io.transition_capacity) {
+          T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
+          for (int j = 0; j < 4; ++j) rec[6 + j] = lo[j];
+          rec[10] = (T)ang;
+          rec[18] = s.n; rec[19] = s.e; rec[20] = s.psi; rec[21] = o_ect;
+          rec[23] = (T)(a.io.env_id_offset + env);
+        }
       }
+      // the observation becomes the next step's state
+      if (type == 0) { lo[0] = s.n; lo[1] = s.e; lo[2] = s.psi; lo[3] = o_rpm; lo[4] = o_ect; lo[5] = o_pme; }
+      else { lo[0] = s.n; lo[1] = s.e; lo[2] = s.psi; lo[3] = o_ect; }
     }
     // episode-done count: one ballot + popcount per wave, one atomic per wave
     if (type == 0 && a.io.done_count) {
@@ -449,10 +489,12 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     }
     // ---------------- auto reset: reset() + init_step() (test_beds/main_ast.py:314-329) ----------------
     if (act) {
-      if (type == 1) ep_step += 1;
+      ep_step += 1;
       if (a.io.auto_reset && env_done) {
         reset_ship(a.sc, type, env, n_env, s, rt.nw);
-        if (type == 1) { samp = T(0); eps = T(0); ep_step = 0; ++episodes; }
+        ep_step = 0;
+        if (type == 1) { samp = T(0); eps = T(0); ++episodes; }
+        for (int j = 0; j < lo_n; ++j) lo[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + lo_base + j];
         init_step_ship(c, s, rt, v_des);
       }
     }
@@ -470,6 +512,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         ge[(size_t)i * n_env] = rt.te[i * kWave];
       }
     }
+    for (int j = 0; j < lo_n; ++j) a.st.last_obs[(size_t)(lo_base + j) * n_env + env] = lo[j];
     if (type == 1) {
       a.st.env[0][env] = samp; a.st.env[1][env] = eps;
       a.st.env[2][env] = ppn; a.st.env[3][env] = ppe;
@@ -521,6 +564,8 @@ __global__ __launch_bounds__(256) void k_reset(const KArgs<T> a, const uint8_t* 
     a.st.env[0][env] = T(0);
     a.st.env[1][env] = T(0);
     a.st.ep_step[env] = 0;
+    for (int j = 0; j < SIT_OBS_DIM; ++j)
+      a.st.last_obs[(size_t)j * n_env + env] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
   }
   // the construction-time observation (constant per env) is returned for every env
   if (initial_state)
@@ -550,6 +595,8 @@ __global__ __launch_bounds__(256) void k_restart(const KArgs<T> a) {
   a.st.ep_step[env] = 0;
   a.st.event[env] = 0;
   a.st.episodes[env] = 0;
+  for (int j = 0; j < SIT_OBS_DIM; ++j)
+    a.st.last_obs[(size_t)j * n_env + env] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
 }
 
 // =======================================================================================
@@ -575,7 +622,10 @@ struct sit_handle {
   unsigned char* map = nullptr;
   int n_poly = 0, n_vert = 0;
   size_t map_off = 0, map_ax = 0, map_ay = 0, map_bx = 0, map_by = 0, map_il2 = 0, map_bbox = 0;
+  size_t map_poly = 0, map_gstart = 0, map_gidx = 0, map_bstart = 0, map_bidx = 0;
   size_t map_bytes = 0;
+  int use_index = 0;
+  double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
   double min_n = 0, max_n = 0, min_e = 0, max_e = 0;
   bool have_map = false, have_routes = false, have_init = false;
 };
@@ -701,6 +751,7 @@ KArgs<T> make_args(const sit_handle* h) {
   a.st.event = reinterpret_cast<uint32_t*>(h->blob + h->off[F_EVENT]);
   a.st.episodes = reinterpret_cast<uint32_t*>(h->blob + h->off[F_EPISODES]);
   a.st.wn = fp(F_WN); a.st.we = fp(F_WE);
+  a.st.last_obs = fp(F_LAST_OBS);
   a.sc.init = reinterpret_cast<const T*>(h->scen + h->scen_init);
   a.sc.end_n = reinterpret_cast<const T*>(h->scen + h->scen_end_n);
   a.sc.end_e = reinterpret_cast<const T*>(h->scen + h->scen_end_e);
@@ -717,6 +768,14 @@ KArgs<T> make_args(const sit_handle* h) {
   a.map.by = reinterpret_cast<const T*>(h->map + h->map_by);
   a.map.inv_len2 = reinterpret_cast<const T*>(h->map + h->map_il2);
   a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
+  a.map.poly = reinterpret_cast<const uint8_t*>(h->map + h->map_poly);
+  a.map.grid_start = reinterpret_cast<const uint16_t*>(h->map + h->map_gstart);
+  a.map.grid_idx = reinterpret_cast<const uint8_t*>(h->map + h->map_gidx);
+  a.map.band_start = reinterpret_cast<const uint16_t*>(h->map + h->map_bstart);
+  a.map.band_idx = reinterpret_cast<const uint8_t*>(h->map + h->map_bidx);
+  a.map.use_index = h->use_index;
+  a.map.gx0 = (T)h->gx0; a.map.gy0 = (T)h->gy0; a.map.ginvx = (T)h->ginvx; a.map.ginvy = (T)h->ginvy;
+  a.map.by0 = (T)h->by0; a.map.binv = (T)h->binv;
   a.map_bytes = (int32_t)h->map_bytes;
   return a;
 }
@@ -852,7 +911,8 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
   size_t off = 0;
   for (int f = 0; f < kNumFields; ++f) {
     int64_t cnt = kFields[f].extent == kShip ? 2LL * n_env
-                 : kFields[f].extent == kEnv ? (int64_t)n_env : 2LL * wpt_capacity * n_env;
+                 : kFields[f].extent == kEnv ? (int64_t)n_env
+                 : kFields[f].extent == kObs ? (int64_t)SIT_OBS_DIM * n_env : 2LL * wpt_capacity * n_env;
     const size_t el = kFields[f].dtype == SIT_DT_REAL ? rs : 4;
     h->off[f] = off;
     h->count[f] = cnt;
@@ -927,6 +987,50 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     const double l2 = ex * ex + ey * ey;
     il2[i] = l2 > 0 ? 1.0 / l2 : 0.0;
   }
+  // ---- spatial index (see sit_device.h): conservative nearest-edge candidates per grid cell,
+  //      edges per horizontal band.  Exact by construction; 1 m slack covers float rounding.
+  std::vector<int> poly_of(nv);
+  for (int p = 0; p < n_poly; ++p)
+    for (int i = offs[p]; i < offs[p + 1]; ++i) poly_of[i] = p;
+  const double ext_x = h->max_e - h->min_e, ext_y = h->max_n - h->min_n;
+  const double mg = 0.1 * std::max(ext_x, ext_y) + 500.0;
+  const double gx0 = h->min_e - mg, gy0 = h->min_n - mg;
+  const double sx = (ext_x + 2 * mg) / kGrid, sy = (ext_y + 2 * mg) / kGrid;
+  const double hd = 0.5 * std::sqrt(sx * sx + sy * sy) + 1.0;
+  auto seg_dist = [&](double px, double py, int i) {
+    const double ex = bxv[i] - vx[i], ey = byv[i] - vy[i], l2 = ex * ex + ey * ey;
+    double t = l2 > 0 ? ((px - vx[i]) * ex + (py - vy[i]) * ey) / l2 : 0.0;
+    t = std::min(1.0, std::max(0.0, t));
+    return std::hypot(px - (vx[i] + t * ex), py - (vy[i] + t * ey));
+  };
+  std::vector<uint16_t> gstart(kGrid * kGrid + 1), bstart(kBands + 1);
+  std::vector<uint8_t> gidx, bidx, poly8(nv);
+  std::vector<double> dcell(nv);
+  for (int j = 0; j < kGrid; ++j)
+    for (int i = 0; i < kGrid; ++i) {
+      const double cx = gx0 + (i + 0.5) * sx, cy = gy0 + (j + 0.5) * sy;
+      double D = INFINITY;
+      for (int e = 0; e < nv; ++e) { dcell[e] = seg_dist(cx, cy, e); D = std::min(D, dcell[e] + hd); }
+      gstart[j * kGrid + i] = (uint16_t)std::min<size_t>(gidx.size(), 65535);
+      for (int e = 0; e < nv; ++e)
+        if (dcell[e] - hd <= D + 1.0) gidx.push_back((uint8_t)e);
+    }
+  gstart[kGrid * kGrid] = (uint16_t)std::min<size_t>(gidx.size(), 65535);
+  const double by0 = h->min_n - 1.0, bh = (ext_y + 2.0) / kBands;
+  for (int b = 0; b < kBands; ++b) {
+    bstart[b] = (uint16_t)std::min<size_t>(bidx.size(), 65535);
+    const double lo = by0 + b * bh - 1.0, hi = by0 + (b + 1) * bh + 1.0;
+    for (int e = 0; e < nv; ++e)
+      if (std::min(vy[e], byv[e]) <= hi && std::max(vy[e], byv[e]) >= lo) bidx.push_back((uint8_t)e);
+  }
+  bstart[kBands] = (uint16_t)std::min<size_t>(bidx.size(), 65535);
+  for (int e = 0; e < nv; ++e) poly8[e] = (uint8_t)poly_of[e];
+  h->use_index = (nv <= 256 && gidx.size() < 65535 && bidx.size() < 65535 &&
+                  gidx.size() + bidx.size() <= 48 * 1024) ? 1 : 0;
+  h->gx0 = gx0; h->gy0 = gy0; h->ginvx = 1.0 / sx; h->ginvy = 1.0 / sy;
+  h->by0 = by0; h->binv = 1.0 / bh;
+  if (!h->use_index) { gidx.assign(1, 0); bidx.assign(1, 0); }
+
   size_t o = 0;
   h->map_off = o; o = align256(o + (n_poly + 1) * 4);
   h->map_ax = o; o = align256(o + nv * rs);
@@ -935,8 +1039,18 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
   h->map_by = o; o = align256(o + nv * rs);
   h->map_il2 = o; o = align256(o + nv * rs);
   h->map_bbox = o; o = align256(o + 4 * n_poly * rs);
+  h->map_poly = o; o = align256(o + nv);
+  h->map_gstart = o; o = align256(o + gstart.size() * 2);
+  h->map_gidx = o; o = align256(o + gidx.size());
+  h->map_bstart = o; o = align256(o + bstart.size() * 2);
+  h->map_bidx = o; o = align256(o + bidx.size());
   std::vector<unsigned char> host(o, 0);
   std::memcpy(host.data() + h->map_off, offs.data(), (n_poly + 1) * 4);
+  std::memcpy(host.data() + h->map_poly, poly8.data(), nv);
+  std::memcpy(host.data() + h->map_gstart, gstart.data(), gstart.size() * 2);
+  std::memcpy(host.data() + h->map_gidx, gidx.data(), gidx.size());
+  std::memcpy(host.data() + h->map_bstart, bstart.data(), bstart.size() * 2);
+  std::memcpy(host.data() + h->map_bidx, bidx.data(), bidx.size());
   auto put = [&](size_t at, const std::vector<double>& src) {
     for (size_t i = 0; i < src.size(); ++i) {
       if (rs == 8) reinterpret_cast<double*>(host.data() + at)[i] = src[i];
@@ -1104,6 +1218,8 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
   if (ra->action_ne && (!ra->sac_update || !ra->init))
     return fail(h, SIT_E_INVALID, "explicit actions need sac_update and init");
   if (ra->env_id_offset < 0) return fail(h, SIT_E_INVALID, "env_id_offset must be >= 0");
+  if (ra->transitions && (!ra->transition_count || ra->transition_capacity <= 0))
+    return fail(h, SIT_E_INVALID, "transitions need transition_count and a positive capacity");
   auto fill = [&](auto* io, auto* tag) {
     using R = std::remove_pointer_t<decltype(tag)>;
     io->n_steps = ra->n_steps; io->auto_reset = ra->auto_reset; io->seed = ra->seed;
@@ -1111,6 +1227,8 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     io->action_ne = (const R*)ra->action_ne; io->sac_update = ra->sac_update; io->init = ra->init;
     io->next_state = (R*)ra->next_state; io->reward = (R*)ra->reward; io->done = ra->done;
     io->status = ra->status; io->action_out = (R*)ra->action_out; io->done_count = ra->done_count;
+    io->transitions = (R*)ra->transitions; io->transition_count = ra->transition_count;
+    io->transition_capacity = ra->transition_capacity; io->mask_horizon = ra->mask_horizon;
   };
   if (h->precision == SIT_F64) {
     StepIO<double> io{};

@@ -92,6 +92,8 @@ class VecMultiShipRLEnv:
         return out
 
     def _field_shape(self, name, count):
+        if name == "last_obs":
+            return (_lib.SIT_OBS_DIM, self.n_env)
         if count == 2 * self.n_env:
             return (2, self.n_env)
         if count == self.n_env:
@@ -148,9 +150,12 @@ class VecMultiShipRLEnv:
 
     def rollout(self, n_steps: int, seed: int = 25450, auto_reset: bool = True, env_id_offset: int = 0,
                 actions: dict | None = None, out: dict | None = None, want=("next_state", "reward", "done",
-                                                                              "status", "action", "done_count")):
+                                                                              "status", "action", "done_count"),
+                transition_capacity: int = 0, mask_horizon: int = 600):
         """K fused steps (one kernel launch).  actions=None: synthetic AST sampler on device.
-        Returns a dict of [K, n_env, ...] tensors (reused from `out` when given)."""
+        Returns a dict of [K, n_env, ...] tensors (reused from `out` when given).  With
+        transition_capacity > 0 the sampling-event replay transitions are appended to
+        out["transitions"] ([capacity, 24]) and counted in out["transition_count"] ([1])."""
         n, K = self.n_env, int(n_steps)
         out = {} if out is None else out
         shapes = {"next_state": ((K, n, _lib.SIT_OBS_DIM), self.dtype), "reward": ((K, n), self.dtype),
@@ -176,6 +181,18 @@ class VecMultiShipRLEnv:
                            ("status", "status"), ("action_out", "action"), ("done_count", "done_count")):
             t = out.get(key) if key in want else None
             setattr(ra, field, None if t is None else t.data_ptr())
+        if transition_capacity > 0:
+            tr = out.get("transitions")
+            if tr is None or tr.shape != (transition_capacity, _lib.SIT_TRANSITION_DIM) or tr.dtype != self.dtype:
+                out["transitions"] = torch.zeros((transition_capacity, _lib.SIT_TRANSITION_DIM),
+                                                 dtype=self.dtype, device=self.device)
+            if out.get("transition_count") is None:
+                out["transition_count"] = torch.zeros(1, dtype=torch.int32, device=self.device)
+            out["transition_count"].zero_()
+            ra.transitions = out["transitions"].data_ptr()
+            ra.transition_count = out["transition_count"].data_ptr()
+            ra.transition_capacity = int(transition_capacity)
+        ra.mask_horizon = int(mask_horizon)
         with torch.cuda.device(self.device):
             _lib.check(self.lib.sit_rollout(self.handle, byref(ra), self._stream()), self.handle)
         return out

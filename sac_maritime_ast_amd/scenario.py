@@ -6,8 +6,9 @@ synthetic routes validated against the island map of test_beds/test_policy.py:18
   test ship  R_test = [[1200,500],[1500,4500],[3500,7000],[7000,9000],[9500,9000]] (north, east)
   obstacle   R_obs  = [[2200,5300],[8600,5200]] (start -> end pair, MSRL_env_ex.py:464)
 Initial state u = v = r = 0, shaft speed 400*pi/30, shaft-speed PI integral 114,
-desired speed 8.5 m/s; for N > 1 envs each ship's start is jittered by +-100 m and +-0.05 rad
-(numpy default_rng(seed)).
+desired speed 8.5 m/s; for N > 1 envs each ship's start is jittered by +-100 m and +-0.05 rad.
+The jitter of env g is a pure function of (seed, g) (splitmix64), so a shard of envs
+[offset, offset + n) on one GPU equals the same envs of a single large run.
 """
 from __future__ import annotations
 
@@ -56,8 +57,27 @@ def heading(a, b):
     return math.atan2(b[1] - a[1], b[0] - a[0])
 
 
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix64(x):
+    x = (x + np.uint64(0x9E3779B97F4A7C15)) & _M64
+    z = x
+    z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & _M64
+    z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & _M64
+    return z ^ (z >> np.uint64(31))
+
+
+def env_uniform(seed: int, env_ids: np.ndarray, k: int) -> np.ndarray:
+    """k-th uniform [0,1) draw of each env id, independent of how envs are sharded."""
+    with np.errstate(over="ignore"):
+        base = _splitmix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ np.uint64(0x5CE7A710))
+        x = _splitmix64(base ^ (env_ids.astype(np.uint64) * np.uint64(0x100000001B3) + np.uint64(k)))
+    return (x >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
 def make_scenario(n_env: int, cap: int = 32, seed: int = 25450, jitter: bool = True,
-                  r_test=R_TEST, r_obs=R_OBS, v_des: float = V_DES) -> Scenario:
+                  r_test=R_TEST, r_obs=R_OBS, v_des: float = V_DES, env_offset: int = 0) -> Scenario:
     routes = np.zeros((n_env, 2, cap, 2))
     routes[:, 0, :len(r_test)] = r_test
     routes[:, 1, :len(r_obs)] = r_obs
@@ -70,8 +90,10 @@ def make_scenario(n_env: int, cap: int = 32, seed: int = 25450, jitter: bool = T
     init[:, :, 6] = OMEGA0
     init[:, :, 7] = v_des
     init[:, :, 9] = SHAFT_PI_I0
-    if jitter and n_env > 1:
-        rng = np.random.default_rng(seed)
-        init[:, :, 0:2] += rng.uniform(-100.0, 100.0, size=(n_env, 2, 2))
-        init[:, :, 2] += rng.uniform(-0.05, 0.05, size=(n_env, 2))
+    if jitter and (n_env > 1 or env_offset > 0):
+        ids = np.arange(env_offset, env_offset + n_env, dtype=np.uint64)
+        for t in range(2):
+            init[:, t, 0] += 200.0 * env_uniform(seed, ids, 3 * t) - 100.0
+            init[:, t, 1] += 200.0 * env_uniform(seed, ids, 3 * t + 1) - 100.0
+            init[:, t, 2] += 0.1 * env_uniform(seed, ids, 3 * t + 2) - 0.05
     return Scenario(routes, n_wpt, init, polygons())

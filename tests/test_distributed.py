@@ -1,0 +1,69 @@
+"""N > 1 path on CPU (gloo, world size 2): env sharding by global env id plus the transition
+all-gather of sac_maritime_ast_amd.shard.  The CPU oracle stands in for the GPU env here; the
+GPU runs use the same shard offsets and the same gather over RCCL."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import sit_oracle as so
+from sac_maritime_ast_amd.scenario import make_scenario
+from sac_maritime_ast_amd.shard import TransitionGather, shard_offset
+
+N_PER_RANK, STEPS, SEED, CAP = 48, 160, 4242, 512
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rollout(n_env, offset):
+    sc = make_scenario(n_env, cap=24, seed=SEED, env_offset=offset)
+    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+    o.reset()
+    o.init_step()
+    return o.rollout(STEPS, seed=SEED, env_id_offset=offset)
+
+
+def _worker(rank, world, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        off = shard_offset(rank, N_PER_RANK)
+        r = _rollout(N_PER_RANK, off)
+        tr = torch.zeros((CAP, 24), dtype=torch.float64)
+        k = min(len(r["transitions"]), CAP)
+        tr[:k] = torch.from_numpy(r["transitions"][:k])
+        cnt = torch.tensor([len(r["transitions"])], dtype=torch.int32)
+        g = TransitionGather(CAP, 24, torch.float64, "cpu", world)
+        g(tr, cnt)
+        ns = torch.from_numpy(r["next_state"])
+        all_ns = [torch.empty_like(ns) for _ in range(world)]
+        dist.all_gather(all_ns, ns)
+        if rank == 0:
+            full = _rollout(world * N_PER_RANK, 0)
+            got = g.records().numpy()
+            want = full["transitions"]
+            assert g.dropped() == 0
+            key = lambda a: np.lexsort((a[:, 12], a[:, 23]))  # noqa: E731
+            got, want = got[key(got)], want[key(want)]
+            assert got.shape == want.shape, (got.shape, want.shape)
+            np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+            sharded = torch.cat(all_ns, dim=1).numpy()
+            np.testing.assert_allclose(sharded, full["next_state"], rtol=1e-12, atol=1e-9)
+            with open(result_path, "w") as f:
+                f.write(f"ok {len(got)}")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_shards_equal_one_big_run(tmp_path):
+    path = str(tmp_path / "result.txt")
+    mp.spawn(_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    assert open(path).read().startswith("ok")
