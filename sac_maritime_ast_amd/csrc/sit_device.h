@@ -68,43 +68,52 @@ struct Consts {
   T bias_scale, bias_max, bias_rudder;
   // reward / termination (MSRL_env_ex.py)
   T e_tol, arrival_radius, rpm_max, min_dist2, theta, blackout_kw, rpm_k, half_len;
+  T inv_dt, inv_e_tol, inv_maxn, inv_jp, inv_r_me, inv_r_hsg;
   T min_n, max_n, min_e, max_e;
   T pi6;
+  // map index geometry (see Map)
+  T gx0, gy0, ginvx, ginvy;   // grid origin and 1 / cell size
+  T by0, binv;                // band origin and 1 / band height
+  T hull_safe;                // half_len * sqrt(2) + 1 m: beyond it all hull corners share the centre's side
 };
 
-// island map: polygon p owns edges [off[p], off[p+1]); edge i runs from (ax, ay) to (bx, by)
-// (ring closed).  Coordinates are (x = east, y = north) as in obstacle.py:128.  The step kernel
-// stages these arrays in LDS once per launch; every lane then reads them as broadcasts.
+// island map (obstacle.py:92-124): edge i of the closed rings runs from (ax, ay) to (bx, by);
+// coordinates are (x = east, y = north) as in obstacle.py:128.  One Edge record per edge (one
+// LDS base pointer, immediate field offsets) so the predicates need no per-array registers.
 //
-// Spatial index (built on the host by sit_load_map, exact by construction):
+// Spatial index (built on the host by sit_load_map, exact by construction), one u16 array:
+//   idx[0 .. G*G]            grid cell starts (absolute positions in idx)
+//   idx[G*G+1 .. G*G+1+NB]   band starts
+//   idx[kClassBase + c]      cell class: 0 = no boundary within 1 m of the cell and its points
+//                            are outside every polygon, 1 = likewise inside one, 2 = mixed
+//   then the entries (edge ids).
 //  * grid: G x G cells over the map extent plus a margin; cell c lists every edge that can be
 //    the nearest edge of some point within 1 m of the cell (conservative bound with a 1 m
 //    float slack), so the minimum over the list equals the minimum over all edges.
 //  * bands: NB horizontal bands; band b lists every edge whose y-range meets the band (+-1 m).
-//    The ray-crossing test of GEOS only ever looks at edges whose y-range contains the
-//    point's y, so scanning the band's list gives the same crossings.
+//    GEOS's ray-crossing test only looks at edges whose y-range contains the point's y.
 constexpr int kGrid = 32;
 constexpr int kBands = 64;
+constexpr int kBandBase = kGrid * kGrid + 1;
+constexpr int kClassBase = kBandBase + kBands + 1;
+
+template <typename T>
+struct alignas(16) Edge {
+  T ax, ay, bx, by;
+  T il2;            // 1 / |edge|^2 (0 for a degenerate edge)
+  uint32_t poly;    // polygon id
+};
 
 template <typename T>
 struct Map {
-  int32_t n_poly;
+  const Edge<T>* edge;      // [n_edge] (LDS copy in the step kernel)
+  const uint16_t* idx;      // packed index (LDS copy in the step kernel)
   int32_t n_edge;
-  int32_t use_index;    // 0: full scans only
-  const int32_t* off;   // [n_poly + 1]
-  const T* ax;          // [n_edge]
-  const T* ay;
-  const T* bx;
-  const T* by;
-  const T* inv_len2;    // [n_edge] 1 / |edge|^2 (0 for a degenerate edge)
-  const T* bbox;        // [n_poly][4] min_x, max_x, min_y, max_y
-  const uint8_t* poly;  // [n_edge] polygon of the edge
-  const uint16_t* grid_start;  // [kGrid * kGrid + 1]
-  const uint8_t* grid_idx;
-  const uint16_t* band_start;  // [kBands + 1]
-  const uint8_t* band_idx;
-  T gx0, gy0, ginvx, ginvy;    // grid origin and 1 / cell size
-  T by0, binv;                 // band origin and 1 / band height
+  int32_t use_index;        // 0: full scans only
+  // fallback scan (global memory): polygon ring offsets and bounding boxes
+  const int32_t* off;       // [n_poly + 1]
+  const T* bbox;            // [n_poly][4] min_x, max_x, min_y, max_y
+  int32_t n_poly;
 };
 
 // --------------------------------------------------------------------------------------
@@ -190,7 +199,7 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
   const T psi_ref = alpha + chi;
   // heading PID, error not wrapped (Q4)
   const T err = psi_ref - s.psi;
-  const T derr = (err - s.hp) / c.dt;
+  const T derr = (err - s.hp) * c.inv_dt;
   s.hi = s.hi + err * c.dt;
   s.hp = err;
   const T out = err * c.kp_h + derr * c.kd_h + s.hi * c.ki_h;
@@ -212,7 +221,7 @@ __device__ __forceinline__ T power_me_kw(const Consts<T>& c, T thr) {
   if (c.sg_mode == 0) load_me = xmin(total, c.me_cap);                  // MOTOR
   else if (c.sg_mode == 1) load_me = total + c.hotel - c.load_el_gen;    // GEN
   else load_me = total;                                                 // OFF
-  return load_me / T(1000);
+  return load_me * T(0.001);
 }
 
 // update_differentials + integrate_differentials (ship_model.py:624-643, ship_engine.py:355-395)
@@ -225,9 +234,10 @@ __device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T 
   const T d_n = cp * u - sp * v;
   const T d_e = sp * u + cp * v;
   // shaft equation with pre-step omega
-  const T tq_me = xmin(thr * c.avail_me / (w + T(0.1)), c.tqcap_me);
-  const T tq_hsg = xmin(thr * c.avail_el / (w + T(0.1)), c.tqcap_el);
-  const T d_w = ((tq_me - c.d_me * w) / c.r_me + (tq_hsg - c.d_hsg * w) / c.r_hsg - c.kp_prop * (w * w)) / c.jp;
+  const T inv_w = T(1) / (w + T(0.1));
+  const T tq_me = xmin(thr * c.avail_me * inv_w, c.tqcap_me);
+  const T tq_hsg = xmin(thr * c.avail_el * inv_w, c.tqcap_el);
+  const T d_w = ((tq_me - c.d_me * w) * c.inv_r_me + (tq_hsg - c.d_hsg * w) * c.inv_r_hsg - c.kp_prop * (w * w)) * c.inv_jp;
   const T thrust = c.thrust_k * w * xabs(w);
   // current in body frame: R(psi)^T v_c
   const T vc_u = cp * c.vc_n + sp * c.vc_e;
@@ -265,9 +275,10 @@ __device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T 
 // --------------------------------------------------------------------------------------
 // polygon predicates (obstacle.py:126-141 -> GEOS)
 // --------------------------------------------------------------------------------------
-// exact sign of a*b - c*d (TwoProduct via fma, Shewchuk grow-expansion)
+// exact sign of a*b - c*d (TwoProduct via fma, Shewchuk grow-expansion); out of line: it
+// only runs when the orientation filter is uncertain
 template <typename T>
-__device__ __forceinline__ int exact_sign_diff(T a, T b, T c, T d) {
+__device__ __attribute__((noinline)) int exact_sign_diff(T a, T b, T c, T d) {
   const T p1 = a * b, e1 = xfma(a, b, -p1);
   const T p2 = c * d, e2 = xfma(c, d, -p2);
   auto two_sum = [](T x, T y, T& err) { const T s = x + y; const T bb = s - x; err = (x - (s - bb)) + (y - bb); return s; };
@@ -300,146 +311,135 @@ __device__ __forceinline__ int orientation(T p1x, T p1y, T p2x, T p2y, T qx, T q
   return exact_sign_diff(ax, by, ay, bx);
 }
 
-// Polygon.contains(Point(e, n)) for any polygon: GEOS RayCrossingCounter (strict interior)
-template <typename T>
-__device__ bool point_in_polys(const Map<T>& m, T n, T e) {
-  const T qx = e, qy = n;
-  bool inside = false;
-  for (int p = 0; p < m.n_poly; ++p) {
-    const T* bb = m.bbox + 4 * p;
-    if (qx < bb[0] || qx > bb[1] || qy < bb[2] || qy > bb[3]) continue;
-    int cross = 0;
-    bool onb = false;
-    for (int i = m.off[p]; i < m.off[p + 1]; ++i) {
-      const T p1x = m.ax[i], p1y = m.ay[i];
-      const T p2x = m.bx[i], p2y = m.by[i];
-      if (p1x < qx && p2x < qx) continue;
-      if (qx == p2x && qy == p2y) { onb = true; break; }
-      if (p1y == qy && p2y == qy) {
-        if (xmin(p1x, p2x) <= qx && qx <= xmax(p1x, p2x)) { onb = true; break; }
-        continue;
-      }
-      if ((p1y > qy && p2y <= qy) || (p2y > qy && p1y <= qy)) {
-        int o = orientation(p1x, p1y, p2x, p2y, qx, qy);
-        if (o == 0) { onb = true; break; }
-        if (p2y < p1y) o = -o;
-        if (o > 0) ++cross;
-      }
-    }
-    inside |= (!onb && (cross & 1));
-  }
-  return inside;
-}
-
-// min over polygons of exterior.distance(Point(e, n)) (GEOS Distance::pointToSegment),
-// evaluated on squared distances with one final sqrt.
-template <typename T>
-__device__ T distance_to_polys(const Map<T>& m, T n, T e) {
-  const T px = e, py = n;
-  T best = T(3.0e38);
-  for (int i = 0; i < m.n_edge; ++i) {
-    const T ax = m.ax[i], ay = m.ay[i];
-    const T bx = m.bx[i], by = m.by[i];
-    const T ex = bx - ax, ey = by - ay;
-    const T qx = px - ax, qy = py - ay;
-    const T t = qx * ex + qy * ey;
-    const T il2 = m.inv_len2[i];
-    T d2;
-    if (il2 == T(0) || t <= T(0)) {
-      d2 = qx * qx + qy * qy;
-    } else if (t * il2 >= T(1)) {
-      const T rx = px - bx, ry = py - by;
-      d2 = rx * rx + ry * ry;
-    } else {
-      const T cr = qy * ex - qx * ey;
-      d2 = cr * cr * il2;
-    }
-    best = xmin(best, d2);
-  }
-  return xsqrt(best);
-}
-
-// squared distance from p to edge i (GEOS Distance::pointToSegment, squared form)
-template <typename T>
-__device__ __forceinline__ T edge_dist2(const Map<T>& m, int i, T px, T py) {
-  const T ax = m.ax[i], ay = m.ay[i];
-  const T ex = m.bx[i] - ax, ey = m.by[i] - ay;
-  const T qx = px - ax, qy = py - ay;
-  const T t = qx * ex + qy * ey;
-  const T il2 = m.inv_len2[i];
-  if (il2 == T(0) || t <= T(0)) return qx * qx + qy * qy;
-  if (t * il2 >= T(1)) {
-    const T rx = px - m.bx[i], ry = py - m.by[i];
-    return rx * rx + ry * ry;
-  }
-  const T cr = qy * ex - qx * ey;
-  return cr * cr * il2;
-}
-
-// distance to the nearest polygon boundary via the grid's candidate lists (same value as
-// distance_to_polys: the lists contain every possible minimiser)
-template <typename T>
-__device__ T distance_indexed(const Map<T>& m, T n, T e) {
-  const T fx = (e - m.gx0) * m.ginvx, fy = (n - m.gy0) * m.ginvy;
-  if (!m.use_index || !(fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)))
-    return distance_to_polys(m, n, e);
-  const int c = (int)fy * kGrid + (int)fx;
-  T best = T(3.0e38);
-  const int k1 = m.grid_start[c + 1];
-  for (int k = m.grid_start[c]; k < k1; ++k) best = xmin(best, edge_dist2(m, m.grid_idx[k], e, n));
-  return xsqrt(best);
-}
-
-// GEOS RayCrossingCounter::countSegment for one segment, per polygon bitmasks
+// GEOS RayCrossingCounter::countSegment for one segment (x = east, y = north), written with
+// predication: the only branch left is the rare exact-orientation fallback.
 template <typename T>
 __device__ __forceinline__ void count_segment(T p1x, T p1y, T p2x, T p2y, T qx, T qy, uint32_t bit,
                                               uint32_t& parity, uint32_t& onb) {
+  // GEOS order: strictly-left segments and the end vertex are resolved first, horizontal
+  // segments never count, straddling segments count when the point is to their left
   if (p1x < qx && p2x < qx) return;
-  if (qx == p2x && qy == p2y) { onb |= bit; return; }
-  if (p1y == qy && p2y == qy) {
-    if (xmin(p1x, p2x) <= qx && qx <= xmax(p1x, p2x)) onb |= bit;
-    return;
-  }
-  if ((p1y > qy && p2y <= qy) || (p2y > qy && p1y <= qy)) {
-    int o = orientation(p1x, p1y, p2x, p2y, qx, qy);
-    if (o == 0) { onb |= bit; return; }
-    if (p2y < p1y) o = -o;
-    if (o > 0) parity ^= bit;
-  }
+  const int up1 = p1y > qy, up2 = p2y > qy;          // above the ray
+  const int eq1 = p1y == qy, eq2 = p2y == qy;
+  const int vertex = (qx == p2x) & eq2;
+  const int horiz = eq1 & eq2;
+  const int on_h = horiz & (xmin(p1x, p2x) <= qx) & (qx <= xmax(p1x, p2x));
+  const int straddle = (up1 & !up2) | (up2 & !up1);   // (p1y > qy && p2y <= qy) || (p2y > qy && p1y <= qy)
+  int o = 0;
+  if (straddle & !vertex) o = orientation(p1x, p1y, p2x, p2y, qx, qy);
+  const int live = straddle & !vertex & !horiz;
+  const int oo = (p2y < p1y) ? -o : o;
+  onb |= (vertex | on_h | (live & (o == 0))) ? bit : 0u;
+  parity ^= (live & (oo > 0)) ? bit : 0u;
 }
 
-// Polygon.contains for two points sharing y (= n): returns bit 0 / bit 1 for x0 / x1
+// Polygon.contains(Point(e, n)) for any polygon by a full scan (fallback path)
 template <typename T>
-__device__ int pip_pair_indexed(const Map<T>& m, T n, T x0, T x1) {
+__device__ bool point_in_polys(const Map<T>& m, T n, T e) {
+  const T qx = e, qy = n;
+  uint32_t par = 0, onb = 0;
+  for (int p = 0; p < m.n_poly; ++p) {
+    const T* bb = m.bbox + 4 * p;
+    if (qx < bb[0] || qx > bb[1] || qy < bb[2] || qy > bb[3]) continue;
+    for (int i = m.off[p]; i < m.off[p + 1]; ++i) {
+      const Edge<T> g = m.edge[i];
+      count_segment(g.ax, g.ay, g.bx, g.by, qx, qy, 1u << g.poly, par, onb);
+    }
+  }
+  return (par & ~onb) != 0;
+}
+
+// squared distance from p to edge g (GEOS Distance::pointToSegment, squared form)
+template <typename T>
+__device__ __forceinline__ T edge_dist2(const Edge<T>& g, T px, T py) {
+  const T ex = g.bx - g.ax, ey = g.by - g.ay;
+  const T qx = px - g.ax, qy = py - g.ay;
+  const T t = qx * ex + qy * ey;
+  const T rx = px - g.bx, ry = py - g.by;
+  const T cr = qy * ex - qx * ey;
+  const T d_a = qx * qx + qy * qy, d_b = rx * rx + ry * ry, d_s = cr * cr * g.il2;
+  return (g.il2 == T(0) || t <= T(0)) ? d_a : (t * g.il2 >= T(1) ? d_b : d_s);
+}
+
+// min over polygons of exterior.distance(Point(e, n)), full scan
+template <typename T>
+__device__ T distance_to_polys(const Map<T>& m, T n, T e) {
+  T best = T(3.0e38);
+  for (int i = 0; i < m.n_edge; ++i) best = xmin(best, edge_dist2(m.edge[i], e, n));
+  return xsqrt(best);
+}
+
+// the same distance via the grid's candidate list
+template <typename T>
+__device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
+  const T fx = (e - c.gx0) * c.ginvx, fy = (n - c.gy0) * c.ginvy;
+  if (!m.use_index || !(fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)))
+    return distance_to_polys(m, n, e);
+  const int cell = (int)fy * kGrid + (int)fx;
+  const int k0 = m.idx[cell], k1 = m.idx[cell + 1];
+  T best = T(3.0e38);
+#pragma unroll 1
+  for (int k = k0; k < k1; ++k) best = xmin(best, edge_dist2(m.edge[m.idx[k]], e, n));
+  return xsqrt(best);
+}
+
+// Polygon.contains for two points sharing y (= n): bit 0 / bit 1 for x0 / x1
+template <typename T>
+__device__ int pip_pair_indexed(const Consts<T>& c, const Map<T>& m, T n, T x0, T x1) {
   if (!m.use_index) return (int)point_in_polys(m, n, x0) | ((int)point_in_polys(m, n, x1) << 1);
-  const T fb = (n - m.by0) * m.binv;
+  const T fb = (n - c.by0) * c.binv;
   if (!(fb >= T(0) && fb < T(kBands))) return 0;   // beyond every edge's y-range
   const int b = (int)fb;
   uint32_t par0 = 0, onb0 = 0, par1 = 0, onb1 = 0;
-  const int k1 = m.band_start[b + 1];
-  for (int k = m.band_start[b]; k < k1; ++k) {
-    const int i = m.band_idx[k];
-    const T p1x = m.ax[i], p1y = m.ay[i], p2x = m.bx[i], p2y = m.by[i];
-    const uint32_t bit = 1u << m.poly[i];
-    count_segment(p1x, p1y, p2x, p2y, x0, n, bit, par0, onb0);
-    count_segment(p1x, p1y, p2x, p2y, x1, n, bit, par1, onb1);
+  const int k0 = m.idx[kBandBase + b], k1 = m.idx[kBandBase + b + 1];
+#pragma unroll 1
+  for (int k = k0; k < k1; ++k) {
+    const Edge<T> g = m.edge[m.idx[k]];
+    const uint32_t bit = 1u << g.poly;
+    count_segment(g.ax, g.ay, g.bx, g.by, x0, n, bit, par0, onb0);
+    count_segment(g.ax, g.ay, g.bx, g.by, x1, n, bit, par1, onb1);
   }
   return ((par0 & ~onb0) != 0 ? 1 : 0) | ((par1 & ~onb1) != 0 ? 2 : 0);
 }
 
 template <typename T>
-__device__ bool pip_indexed(const Map<T>& m, T n, T e) {
+__device__ bool pip_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   if (!m.use_index) return point_in_polys(m, n, e);
-  const T fb = (n - m.by0) * m.binv;
+  const T fb = (n - c.by0) * c.binv;
   if (!(fb >= T(0) && fb < T(kBands))) return false;
   const int b = (int)fb;
   uint32_t par = 0, onb = 0;
-  const int k1 = m.band_start[b + 1];
-  for (int k = m.band_start[b]; k < k1; ++k) {
-    const int i = m.band_idx[k];
-    count_segment(m.ax[i], m.ay[i], m.bx[i], m.by[i], e, n, 1u << m.poly[i], par, onb);
+  const int k0 = m.idx[kBandBase + b], k1 = m.idx[kBandBase + b + 1];
+#pragma unroll 1
+  for (int k = k0; k < k1; ++k) {
+    const Edge<T> g = m.edge[m.idx[k]];
+    count_segment(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
   }
   return (par & ~onb) != 0;
+}
+
+// Polygon.contains(Point(e, n)): grid-cell class when the cell is pure, band scan otherwise
+template <typename T>
+__device__ bool pip_point(const Consts<T>& c, const Map<T>& m, T n, T e) {
+  if (m.use_index) {
+    const T fx = (e - c.gx0) * c.ginvx, fy = (n - c.gy0) * c.ginvy;
+    if (fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)) {
+      const int cls = m.idx[kClassBase + (int)fy * kGrid + (int)fx];
+      if (cls < 2) return cls == 1;
+    }
+  }
+  return pip_indexed(c, m, n, e);
+}
+
+// is_pos_inside_obstacles (MSRL_env_ex.py:490-515): any of the 4 corners (n +- h, e +- h)
+// strictly inside a polygon.  When the centre is farther than h*sqrt(2) + 1 m from every
+// boundary (dobst: the reward's distance), no corner-centre segment meets a boundary, so all
+// corners share the centre's side and one point test decides.
+template <typename T>
+__device__ bool hull_in_terrain(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst) {
+  if (dobst > c.hull_safe) return pip_point(c, m, n, e);
+  const T h = c.half_len;
+  return (pip_pair_indexed(c, m, n - h, e - h, e + h) | pip_pair_indexed(c, m, n + h, e - h, e + h)) != 0;
 }
 
 }  // namespace sit

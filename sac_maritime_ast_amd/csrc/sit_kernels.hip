@@ -127,29 +127,17 @@ struct KArgs {
   int32_t map_bytes;
 };
 
-// Copy the map blob (offsets, edge arrays, bboxes: one contiguous allocation) into LDS at
-// `dst` and return a Map whose pointers address the LDS copy.
+// Copy the edge records and the packed index (the first map_bytes of the map blob, which
+// starts with Edge[n_edge] followed by the u16 index) into LDS at `dst`.
 template <typename T>
 __device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* dst) {
-  const unsigned char* src = reinterpret_cast<const unsigned char*>(a.map.off);
+  const unsigned char* src = reinterpret_cast<const unsigned char*>(a.map.edge);
   const int n16 = a.map_bytes / 16;
   for (int i = threadIdx.x; i < n16; i += blockDim.x)
     reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-  auto rebase = [&](const auto* p) {
-    using P = std::remove_cv_t<std::remove_pointer_t<decltype(p)>>;
-    return reinterpret_cast<const P*>(dst + (reinterpret_cast<const unsigned char*>(p) - src));
-  };
   Map<T> m = a.map;
-  m.off = rebase(a.map.off);
-  m.ax = rebase(a.map.ax); m.ay = rebase(a.map.ay);
-  m.bx = rebase(a.map.bx); m.by = rebase(a.map.by);
-  m.inv_len2 = rebase(a.map.inv_len2);
-  m.bbox = rebase(a.map.bbox);
-  m.poly = rebase(a.map.poly);
-  m.grid_start = rebase(a.map.grid_start);
-  m.grid_idx = rebase(a.map.grid_idx);
-  m.band_start = rebase(a.map.band_start);
-  m.band_idx = rebase(a.map.band_idx);
+  m.edge = reinterpret_cast<const Edge<T>*>(dst);
+  m.idx = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.idx) - src));
   return m;
 }
 
@@ -215,14 +203,6 @@ __device__ __forceinline__ bool outside(const Consts<T>& c, T n, T e, T margin) 
   return n < c.min_n + margin || n > c.max_n - margin || e < c.min_e + margin || e > c.max_e - margin;
 }
 
-// is_pos_inside_obstacles: 4 corners of a +-l/2 square (MSRL_env_ex.py:490-515); the two
-// corners of one side share a y and one band scan
-template <typename T>
-__device__ __forceinline__ bool hull_in_terrain(const Consts<T>& c, const Map<T>& m, T n, T e) {
-  const T h = c.half_len;
-  return (pip_pair_indexed(m, n - h, e - h, e + h) | pip_pair_indexed(m, n + h, e - h, e + h)) != 0;
-}
-
 constexpr uint32_t kStopBit = 1u << 30;   // exchange-only: stop flag after this ship's checks
 constexpr uint32_t kDoneBit = 1u << 29;   // exchange-only: this ship's done
 
@@ -245,7 +225,13 @@ template <typename T, bool SYNTH, bool STAGE>
 __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Xchg<T> xs[2];
-  const Consts<T>& c = a.c;
+  // The ~70 per-step constants are read from a block copy in LDS: loads from LDS land in
+  // VGPRs (one wave per SIMD leaves plenty), whereas kernel-argument constants compete for
+  // the 102 SGPRs and spill to VGPR lanes (v_readlane in the loop).
+  __shared__ Consts<T> cs;
+  for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
+    reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
+  const Consts<T>& c = cs;
   // LDS: [map blob][route tables if STAGE]
   const Map<T> map = stage_map(a, smem);
   unsigned char* route_lds = smem + ((a.map_bytes + 255) & ~255);
@@ -346,7 +332,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           const T pre_n = s.n, pre_e = s.e;
           T rudder, thr;
           guidance_control(c, s, rt, v_des, rudder, thr, o_ect);
-          o_rpm = s.w * T(30) / T(M_PI);
+          o_rpm = s.w * c.rpm_k;
           o_pme = power_me_kw(c, thr);
           s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
           ship_dynamics(c, s, thr, rudder);
@@ -367,7 +353,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
           rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
         }
-        o_rpm = s.w * T(30) / T(M_PI);
+        o_rpm = s.w * c.rpm_k;
         o_pme = power_me_kw(c, thr);
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
         ship_dynamics(c, s, thr, rudder);
@@ -375,15 +361,20 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       }
 
       // ---------------- own termination predicates (MSRL_env_ex.py:628-881) ----------------
-      const T dobst = distance_indexed(map, s.n, s.e);
+#ifdef SIT_ABLATE_PREDICATES   // diagnostic builds only (tools/ablate.sh): polygon work removed
+      const T dobst = T(1000);
+      const bool terrain = false;
+#else
+      const T dobst = distance_indexed(c, map, s.n, s.e);
+      const bool terrain = hull_in_terrain(c, map, s.n, s.e, dobst);
+#endif
       const T dn_end = s.n - rt.end_n, de_end = s.e - rt.end_e;
       const bool arrive = xsqrt(dn_end * dn_end + de_end * de_end) <= c.arrival_radius;
       const bool horizon = outside(c, s.n, s.e, c.half_len);
-      const bool terrain = hull_in_terrain(c, map, s.n, s.e);
       int stop = s.stop;
       bool done = false;
       if (type == 0) {
-        r_nt = xabs(o_ect) / c.e_tol + (T(1) - dobst / maxn) / T(100);
+        r_nt = xabs(o_ect) * c.inv_e_tol + (T(1) - dobst * c.inv_maxn) * T(0.01);
         const bool pred[6] = {arrive, horizon, terrain, xabs(o_rpm) > c.rpm_max, xabs(o_ect) > c.e_tol,
                               o_pme > c.blackout_kw};
         const T rew[6] = {T(0), T(0), T(1000), T(1000), T(1000), T(1000)};
@@ -399,7 +390,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         if (done) bits |= SIT_ST_TEST_DONE;
       } else {
         if (!stop)
-          r_nt = T(0.1) + (-(xabs(o_ect) / c.e_tol)) / T(100) + (-(T(1) - dobst / maxn)) / T(100);
+          r_nt = T(0.1) - xabs(o_ect) * c.inv_e_tol * T(0.01) - (T(1) - dobst * c.inv_maxn) * T(0.01);
         if (arrive) { stop = 1; bits |= SIT_ST_OBS_ENDPOINT; }
         if (horizon) { stop = 1; done = true; bits |= SIT_ST_OBS_HORIZON; }
         if (terrain) {                   // done without stop flag (Q12)
@@ -407,7 +398,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           done = true;
           bits |= SIT_ST_OBS_TERRAIN;
         }
-        if (outside(c, iwn, iwe, T(0)) || pip_indexed(map, iwn, iwe)) {   // Q11
+#ifdef SIT_ABLATE_PREDICATES
+        if (outside(c, iwn, iwe, T(0))) {
+#else
+        if (outside(c, iwn, iwe, T(0)) || pip_point(c, map, iwn, iwe)) {   // Q11
+#endif
           if (!stop) r_term = r_term - T(1000);
           stop = 1; done = true;
           bits |= SIT_ST_OBS_IW_TERMINAL;
@@ -440,7 +435,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       env_done = ((bt | bo) & kDoneBit) || coll;
       if (coll) s.stop = 1;
       if (type == 0) {
-        const T r_snt = (bo & kStopBit) ? T(0) : (T(1) - xsqrt(dn * dn + de * de) / maxn) / T(1000);
+        const T r_snt = (bo & kStopBit) ? T(0) : (T(1) - xsqrt(dn * dn + de * de) * c.inv_maxn) * T(0.001);
         const T rs = coll ? T(2000) : T(0);
         const T reward = r_nt + r_term + x.r_nto[lane] + x.r_o[lane] + r_snt + rs;
         const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
@@ -621,9 +616,8 @@ struct sit_handle {
   // map
   unsigned char* map = nullptr;
   int n_poly = 0, n_vert = 0;
-  size_t map_off = 0, map_ax = 0, map_ay = 0, map_bx = 0, map_by = 0, map_il2 = 0, map_bbox = 0;
-  size_t map_poly = 0, map_gstart = 0, map_gidx = 0, map_bstart = 0, map_bidx = 0;
-  size_t map_bytes = 0;
+  size_t map_idx = 0, map_off = 0, map_bbox = 0;
+  size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
   double min_n = 0, max_n = 0, min_e = 0, max_e = 0;
@@ -730,9 +724,18 @@ Consts<T> make_consts(const sit_handle* h) {
   c.theta = (T)p.theta;
   c.blackout_kw = (T)(me / 1000);
   c.rpm_k = (T)(30.0 / M_PI);
+  c.inv_dt = (T)(1.0 / p.integration_step);
+  c.inv_e_tol = (T)(1.0 / p.e_tolerance);
+  c.inv_maxn = (T)(1.0 / h->max_n);
+  c.inv_jp = (T)(1.0 / p.propeller_inertia);
+  c.inv_r_me = (T)(1.0 / p.gear_ratio_between_main_engine_and_propeller);
+  c.inv_r_hsg = (T)(1.0 / p.gear_ratio_between_hybrid_shaft_generator_and_propeller);
   c.half_len = (T)(l / 2);
   c.min_n = (T)h->min_n; c.max_n = (T)h->max_n; c.min_e = (T)h->min_e; c.max_e = (T)h->max_e;
   c.pi6 = (T)(M_PI / 6.0);
+  c.gx0 = (T)h->gx0; c.gy0 = (T)h->gy0; c.ginvx = (T)h->ginvx; c.ginvy = (T)h->ginvy;
+  c.by0 = (T)h->by0; c.binv = (T)h->binv;
+  c.hull_safe = (T)(l / 2 * std::sqrt(2.0) + 1.0);
   return c;
 }
 
@@ -761,21 +764,11 @@ KArgs<T> make_args(const sit_handle* h) {
   a.sc.initial_state = reinterpret_cast<const T*>(h->scen + h->scen_initial);
   a.map.n_poly = h->n_poly;
   a.map.n_edge = h->n_vert;
-  a.map.off = reinterpret_cast<const int32_t*>(h->map + h->map_off);
-  a.map.ax = reinterpret_cast<const T*>(h->map + h->map_ax);
-  a.map.ay = reinterpret_cast<const T*>(h->map + h->map_ay);
-  a.map.bx = reinterpret_cast<const T*>(h->map + h->map_bx);
-  a.map.by = reinterpret_cast<const T*>(h->map + h->map_by);
-  a.map.inv_len2 = reinterpret_cast<const T*>(h->map + h->map_il2);
-  a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
-  a.map.poly = reinterpret_cast<const uint8_t*>(h->map + h->map_poly);
-  a.map.grid_start = reinterpret_cast<const uint16_t*>(h->map + h->map_gstart);
-  a.map.grid_idx = reinterpret_cast<const uint8_t*>(h->map + h->map_gidx);
-  a.map.band_start = reinterpret_cast<const uint16_t*>(h->map + h->map_bstart);
-  a.map.band_idx = reinterpret_cast<const uint8_t*>(h->map + h->map_bidx);
   a.map.use_index = h->use_index;
-  a.map.gx0 = (T)h->gx0; a.map.gy0 = (T)h->gy0; a.map.ginvx = (T)h->ginvx; a.map.ginvy = (T)h->ginvy;
-  a.map.by0 = (T)h->by0; a.map.binv = (T)h->binv;
+  a.map.edge = reinterpret_cast<const Edge<T>*>(h->map);
+  a.map.idx = reinterpret_cast<const uint16_t*>(h->map + h->map_idx);
+  a.map.off = reinterpret_cast<const int32_t*>(h->map + h->map_off);
+  a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
   a.map_bytes = (int32_t)h->map_bytes;
   return a;
 }
@@ -1003,66 +996,91 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     t = std::min(1.0, std::max(0.0, t));
     return std::hypot(px - (vx[i] + t * ex), py - (vy[i] + t * ey));
   };
-  std::vector<uint16_t> gstart(kGrid * kGrid + 1), bstart(kBands + 1);
-  std::vector<uint8_t> gidx, bidx, poly8(nv);
+  // packed u16 index: [grid starts (G*G+1)][band starts (NB+1)][entries]
+  std::vector<uint16_t> gentries, bentries;
+  std::vector<uint32_t> gstart(kGrid * kGrid + 1), bstart(kBands + 1);
   std::vector<double> dcell(nv);
   for (int j = 0; j < kGrid; ++j)
     for (int i = 0; i < kGrid; ++i) {
       const double cx = gx0 + (i + 0.5) * sx, cy = gy0 + (j + 0.5) * sy;
       double D = INFINITY;
       for (int e = 0; e < nv; ++e) { dcell[e] = seg_dist(cx, cy, e); D = std::min(D, dcell[e] + hd); }
-      gstart[j * kGrid + i] = (uint16_t)std::min<size_t>(gidx.size(), 65535);
+      gstart[j * kGrid + i] = (uint32_t)gentries.size();
       for (int e = 0; e < nv; ++e)
-        if (dcell[e] - hd <= D + 1.0) gidx.push_back((uint8_t)e);
+        if (dcell[e] - hd <= D + 1.0) gentries.push_back((uint16_t)e);
     }
-  gstart[kGrid * kGrid] = (uint16_t)std::min<size_t>(gidx.size(), 65535);
+  gstart[kGrid * kGrid] = (uint32_t)gentries.size();
   const double by0 = h->min_n - 1.0, bh = (ext_y + 2.0) / kBands;
   for (int b = 0; b < kBands; ++b) {
-    bstart[b] = (uint16_t)std::min<size_t>(bidx.size(), 65535);
+    bstart[b] = (uint32_t)bentries.size();
     const double lo = by0 + b * bh - 1.0, hi = by0 + (b + 1) * bh + 1.0;
     for (int e = 0; e < nv; ++e)
-      if (std::min(vy[e], byv[e]) <= hi && std::max(vy[e], byv[e]) >= lo) bidx.push_back((uint8_t)e);
+      if (std::min(vy[e], byv[e]) <= hi && std::max(vy[e], byv[e]) >= lo) bentries.push_back((uint16_t)e);
   }
-  bstart[kBands] = (uint16_t)std::min<size_t>(bidx.size(), 65535);
-  for (int e = 0; e < nv; ++e) poly8[e] = (uint8_t)poly_of[e];
-  h->use_index = (nv <= 256 && gidx.size() < 65535 && bidx.size() < 65535 &&
-                  gidx.size() + bidx.size() <= 48 * 1024) ? 1 : 0;
+  bstart[kBands] = (uint32_t)bentries.size();
+  // cell classes: pure cells (no boundary within 1 m of the cell) take the side of their centre
+  std::vector<uint16_t> cls(kGrid * kGrid, 2);
+  auto inside_center = [&](double px, double py) {   // crossing number; the point is >= 1 m off every edge
+    bool in = false;
+    for (int p = 0; p < n_poly; ++p) {
+      int cross = 0;
+      for (int i = offs[p]; i < offs[p + 1]; ++i) {
+        const double x1 = vx[i], y1 = vy[i], x2 = bxv[i], y2 = byv[i];
+        if ((y1 > py) != (y2 > py)) {
+          const double xi = x1 + (py - y1) * (x2 - x1) / (y2 - y1);
+          if (xi > px) ++cross;
+        }
+      }
+      in |= (cross & 1) != 0;
+    }
+    return in;
+  };
+  for (int j = 0; j < kGrid; ++j)
+    for (int i = 0; i < kGrid; ++i) {
+      const double cx = gx0 + (i + 0.5) * sx, cy = gy0 + (j + 0.5) * sy;
+      double dmin = INFINITY;
+      for (int e = 0; e < nv; ++e) dmin = std::min(dmin, seg_dist(cx, cy, e));
+      if (dmin > hd + 1.0) cls[j * kGrid + i] = inside_center(cx, cy) ? 1 : 0;
+    }
+  const size_t head = (size_t)kClassBase + kGrid * kGrid;
+  const size_t n_idx = head + gentries.size() + bentries.size();
+  h->use_index = (n_idx < 65535 && n_idx * 2 <= 48 * 1024) ? 1 : 0;
   h->gx0 = gx0; h->gy0 = gy0; h->ginvx = 1.0 / sx; h->ginvy = 1.0 / sy;
   h->by0 = by0; h->binv = 1.0 / bh;
-  if (!h->use_index) { gidx.assign(1, 0); bidx.assign(1, 0); }
-
-  size_t o = 0;
+  std::vector<uint16_t> idx(h->use_index ? n_idx : 2, 0);
+  if (h->use_index) {
+    for (int c = 0; c <= kGrid * kGrid; ++c) idx[c] = (uint16_t)(head + gstart[c]);
+    for (int b = 0; b <= kBands; ++b) idx[kBandBase + b] = (uint16_t)(head + gentries.size() + bstart[b]);
+    std::copy(cls.begin(), cls.end(), idx.begin() + kClassBase);
+    std::copy(gentries.begin(), gentries.end(), idx.begin() + head);
+    std::copy(bentries.begin(), bentries.end(), idx.begin() + head + gentries.size());
+  }
+  // blob: [Edge<T>[nv]][u16 index] (staged into LDS) [ring offsets][bboxes] (fallback, global)
+  const size_t esz = rs == 8 ? sizeof(Edge<double>) : sizeof(Edge<float>);
+  size_t o = align256(nv * esz);
+  h->map_idx = o; o = align256(o + idx.size() * 2);
+  h->map_bytes = o;
   h->map_off = o; o = align256(o + (n_poly + 1) * 4);
-  h->map_ax = o; o = align256(o + nv * rs);
-  h->map_ay = o; o = align256(o + nv * rs);
-  h->map_bx = o; o = align256(o + nv * rs);
-  h->map_by = o; o = align256(o + nv * rs);
-  h->map_il2 = o; o = align256(o + nv * rs);
   h->map_bbox = o; o = align256(o + 4 * n_poly * rs);
-  h->map_poly = o; o = align256(o + nv);
-  h->map_gstart = o; o = align256(o + gstart.size() * 2);
-  h->map_gidx = o; o = align256(o + gidx.size());
-  h->map_bstart = o; o = align256(o + bstart.size() * 2);
-  h->map_bidx = o; o = align256(o + bidx.size());
   std::vector<unsigned char> host(o, 0);
-  std::memcpy(host.data() + h->map_off, offs.data(), (n_poly + 1) * 4);
-  std::memcpy(host.data() + h->map_poly, poly8.data(), nv);
-  std::memcpy(host.data() + h->map_gstart, gstart.data(), gstart.size() * 2);
-  std::memcpy(host.data() + h->map_gidx, gidx.data(), gidx.size());
-  std::memcpy(host.data() + h->map_bstart, bstart.data(), bstart.size() * 2);
-  std::memcpy(host.data() + h->map_bidx, bidx.data(), bidx.size());
-  auto put = [&](size_t at, const std::vector<double>& src) {
-    for (size_t i = 0; i < src.size(); ++i) {
-      if (rs == 8) reinterpret_cast<double*>(host.data() + at)[i] = src[i];
-      else reinterpret_cast<float*>(host.data() + at)[i] = (float)src[i];
+  for (int e = 0; e < nv; ++e) {
+    if (rs == 8) {
+      Edge<double> g{vx[e], vy[e], bxv[e], byv[e], il2[e], (uint32_t)poly_of[e]};
+      std::memcpy(host.data() + e * esz, &g, sizeof(g));
+    } else {
+      Edge<float> g{(float)vx[e], (float)vy[e], (float)bxv[e], (float)byv[e], (float)il2[e], (uint32_t)poly_of[e]};
+      std::memcpy(host.data() + e * esz, &g, sizeof(g));
     }
-  };
-  put(h->map_ax, vx); put(h->map_ay, vy); put(h->map_bx, bxv); put(h->map_by, byv);
-  put(h->map_il2, il2); put(h->map_bbox, bbox);
+  }
+  std::memcpy(host.data() + h->map_idx, idx.data(), idx.size() * 2);
+  std::memcpy(host.data() + h->map_off, offs.data(), (n_poly + 1) * 4);
+  for (size_t i = 0; i < bbox.size(); ++i) {
+    if (rs == 8) reinterpret_cast<double*>(host.data() + h->map_bbox)[i] = bbox[i];
+    else reinterpret_cast<float*>(host.data() + h->map_bbox)[i] = (float)bbox[i];
+  }
   if (h->map) { (void)hipFree(h->map); h->map = nullptr; }
   HIP_TRY(h, hipMalloc(&h->map, o));
   HIP_TRY(h, hipMemcpy(h->map, host.data(), o, hipMemcpyHostToDevice));
-  h->map_bytes = o;
   h->n_poly = n_poly;
   h->n_vert = nv;
   h->have_map = true;
