@@ -75,6 +75,7 @@ struct Consts {
   T gx0, gy0, ginvx, ginvy;   // grid origin and 1 / cell size
   T by0, binv;                // band origin and 1 / band height
   T hull_safe;                // half_len * sqrt(2) + 1 m: beyond it all hull corners share the centre's side
+  T fx0, fy0, finvx, finvy;   // fine class grid origin and 1 / cell size
 };
 
 // island map (obstacle.py:92-124): edge i of the closed rings runs from (ax, ay) to (bx, by);
@@ -84,18 +85,23 @@ struct Consts {
 // Spatial index (built on the host by sit_load_map, exact by construction), one u16 array:
 //   idx[0 .. G*G]            grid cell starts (absolute positions in idx)
 //   idx[G*G+1 .. G*G+1+NB]   band starts
-//   idx[kClassBase + c]      cell class: 0 = no boundary within 1 m of the cell and its points
-//                            are outside every polygon, 1 = likewise inside one, 2 = mixed
 //   then the entries (edge ids).
 //  * grid: G x G cells over the map extent plus a margin; cell c lists every edge that can be
 //    the nearest edge of some point within 1 m of the cell (conservative bound with a 1 m
 //    float slack), so the minimum over the list equals the minimum over all edges.
 //  * bands: NB horizontal bands; band b lists every edge whose y-range meets the band (+-1 m).
 //    GEOS's ray-crossing test only looks at edges whose y-range contains the point's y.
+//  * classes (separate u32 array): kFine x kFine cells over the map extent + 100 m, 2 bits per
+//    cell: 0 = no boundary within 1 m of the cell and its points are outside every polygon,
+//    1 = likewise inside one, 2 = mixed.  A point outside the class grid is > 100 m off the
+//    map and therefore outside every polygon.  With ~40 m cells every point farther than
+//    ~31 m from the shore resolves by one lookup.
 constexpr int kGrid = 32;
 constexpr int kBands = 64;
 constexpr int kBandBase = kGrid * kGrid + 1;
-constexpr int kClassBase = kBandBase + kBands + 1;
+constexpr int kIdxHead = kBandBase + kBands + 1;
+constexpr int kFine = 256;
+constexpr int kFineWords = kFine * kFine / 16;
 
 template <typename T>
 struct alignas(16) Edge {
@@ -108,6 +114,7 @@ template <typename T>
 struct Map {
   const Edge<T>* edge;      // [n_edge] (LDS copy in the step kernel)
   const uint16_t* idx;      // packed index (LDS copy in the step kernel)
+  const uint32_t* fine;     // [kFineWords] 2-bit cell classes (LDS copy in the step kernel)
   int32_t n_edge;
   int32_t use_index;        // 0: full scans only
   // fallback scan (global memory): polygon ring offsets and bounding boxes
@@ -144,6 +151,9 @@ __device__ __forceinline__ double sampler_uniform(uint64_t seed, uint64_t env_id
 // [cap][stride] table (global or LDS); the final waypoint is held in registers because
 // insertion happens at index -1 (controllers.py:298-303) and never moves it.
 // --------------------------------------------------------------------------------------
+//
+// The active leg (waypoints k-1 and k) is cached in registers: the table is read only when k
+// advances or the route is reloaded, and written only by an insertion, so it stays in HBM.
 template <typename T>
 struct Route {
   T* tn;          // column base: entry i at tn[i * stride]
@@ -151,8 +161,21 @@ struct Route {
   int stride;
   T end_n, end_e;
   int nw;         // current number of waypoints
+  T pn, pe;       // waypoint k-1
+  T cn, ce;       // waypoint k
   __device__ __forceinline__ T n(int i) const { return (i >= nw - 1) ? end_n : tn[i * stride]; }
   __device__ __forceinline__ T e(int i) const { return (i >= nw - 1) ? end_e : te[i * stride]; }
+  __device__ __forceinline__ void load_leg(int k) { pn = n(k - 1); pe = e(k - 1); cn = n(k); ce = e(k); }
+  // update_route: insert (in_, ie) at index -1 (controllers.py:298-303); false on overflow
+  __device__ __forceinline__ bool insert(T in_, T ie, int k, int cap) {
+    if (nw >= cap) return false;
+    const int i = nw - 1;
+    tn[i * stride] = in_;
+    te[i * stride] = ie;
+    nw += 1;
+    if (k == i) { cn = in_; ce = ie; }   // the leg pointed at the final waypoint
+    return true;
+  }
 };
 
 // --------------------------------------------------------------------------------------
@@ -173,18 +196,22 @@ struct Ship {
 // rudder_angle_from_sampled_route + throttle (controllers.py:306-314, 138-143, 52-62, 81-93,
 // 180-189; LOS_guidance.py:88-121).  Returns rudder, throttle and |e_ct|.
 template <typename T>
-__device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s, const Route<T>& rt,
+__device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s, Route<T>& rt,
                                                  T v_des, T& rudder, T& thr, T& ect_abs) {
   // next_wpt: acceptance test evaluated in double, without contraction, from the stored
   // values (bit-identical to the float64 reference for identical inputs)
   {
-    const double dn = (double)rt.n(s.k) - (double)s.n;
-    const double de = (double)rt.e(s.k) - (double)s.e;
+    const double dn = (double)rt.cn - (double)s.n;
+    const double de = (double)rt.ce - (double)s.e;
     const double d2 = __dadd_rn(__dmul_rn(dn, dn), __dmul_rn(de, de));
-    if (d2 <= c.ra2 && rt.nw > s.k + 1) s.k += 1;
+    if (d2 <= c.ra2 && rt.nw > s.k + 1) {
+      s.k += 1;
+      rt.pn = rt.cn; rt.pe = rt.ce;
+      rt.cn = rt.n(s.k); rt.ce = rt.e(s.k);
+    }
   }
-  const T pn = rt.n(s.k - 1), pe = rt.e(s.k - 1);
-  const T dx = rt.n(s.k) - pn, dy = rt.e(s.k) - pe;
+  const T pn = rt.pn, pe = rt.pe;
+  const T dx = rt.cn - pn, dy = rt.ce - pe;
   const T alpha = xatan2(dy, dx);
   const T len = xsqrt(dx * dx + dy * dy);
   T sa = T(0), ca = T(1);
@@ -418,16 +445,20 @@ __device__ bool pip_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   return (par & ~onb) != 0;
 }
 
-// Polygon.contains(Point(e, n)): grid-cell class when the cell is pure, band scan otherwise
+// class of a point from the class grid: 0 out, 1 in, 2 mixed (built for every map)
+template <typename T>
+__device__ __forceinline__ int fine_class(const Consts<T>& c, const Map<T>& m, T n, T e) {
+  const T fx = (e - c.fx0) * c.finvx, fy = (n - c.fy0) * c.finvy;
+  if (!(fx >= T(0) && fx < T(kFine) && fy >= T(0) && fy < T(kFine))) return 0;
+  const int cell = (int)fy * kFine + (int)fx;
+  return (m.fine[cell >> 4] >> ((cell & 15) * 2)) & 3;
+}
+
+// Polygon.contains(Point(e, n)): fine-grid class when the cell is pure, band scan otherwise
 template <typename T>
 __device__ bool pip_point(const Consts<T>& c, const Map<T>& m, T n, T e) {
-  if (m.use_index) {
-    const T fx = (e - c.gx0) * c.ginvx, fy = (n - c.gy0) * c.ginvy;
-    if (fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)) {
-      const int cls = m.idx[kClassBase + (int)fy * kGrid + (int)fx];
-      if (cls < 2) return cls == 1;
-    }
-  }
+  const int cls = fine_class(c, m, n, e);
+  if (cls < 2) return cls == 1;
   return pip_indexed(c, m, n, e);
 }
 
@@ -439,7 +470,14 @@ template <typename T>
 __device__ bool hull_in_terrain(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst) {
   if (dobst > c.hull_safe) return pip_point(c, m, n, e);
   const T h = c.half_len;
-  return (pip_pair_indexed(c, m, n - h, e - h, e + h) | pip_pair_indexed(c, m, n + h, e - h, e + h)) != 0;
+  // near shore: each corner by its fine-grid class, band scans only for corners in mixed cells
+  const int c00 = fine_class(c, m, n - h, e - h), c01 = fine_class(c, m, n - h, e + h);
+  const int c10 = fine_class(c, m, n + h, e - h), c11 = fine_class(c, m, n + h, e + h);
+  if (c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1) return true;
+  bool hit = false;
+  if (c00 >= 2 || c01 >= 2) hit |= pip_pair_indexed(c, m, n - h, e - h, e + h) != 0;
+  if (c10 >= 2 || c11 >= 2) hit |= pip_pair_indexed(c, m, n + h, e - h, e + h) != 0;
+  return hit;
 }
 
 }  // namespace sit

@@ -127,8 +127,8 @@ struct KArgs {
   int32_t map_bytes;
 };
 
-// Copy the edge records and the packed index (the first map_bytes of the map blob, which
-// starts with Edge[n_edge] followed by the u16 index) into LDS at `dst`.
+// Copy the edge records, the packed index and the class grid (the first map_bytes of the map
+// blob) into LDS at `dst`.
 template <typename T>
 __device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* dst) {
   const unsigned char* src = reinterpret_cast<const unsigned char*>(a.map.edge);
@@ -138,6 +138,7 @@ __device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* ds
   Map<T> m = a.map;
   m.edge = reinterpret_cast<const Edge<T>*>(dst);
   m.idx = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.idx) - src));
+  m.fine = reinterpret_cast<const uint32_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.fine) - src));
   return m;
 }
 
@@ -191,7 +192,7 @@ __device__ __forceinline__ void reset_ship(const Scen<T>& sc, int type, int env,
 
 // one guidance/control/update/integrate cycle without store, time or bias (MSRL_Env.py:190-217)
 template <typename T>
-__device__ __forceinline__ void init_step_ship(const Consts<T>& c, Ship<T>& s, const Route<T>& rt, T v_des) {
+__device__ __forceinline__ void init_step_ship(const Consts<T>& c, Ship<T>& s, Route<T>& rt, T v_des) {
   T rudder, thr, ect;
   guidance_control(c, s, rt, v_des, rudder, thr, ect);
   ship_dynamics(c, s, thr, rudder);
@@ -219,9 +220,8 @@ struct Xchg {
 // ---------------------------------------------------------------------------------------
 // the env step kernel: K steps of MultiShipRLEnv.step (+ optional auto-reset)
 //   SYNTH : actions from the synthetic AST sampler (else explicit arrays)
-//   STAGE : route tables staged in LDS for the K steps (else read in place from HBM)
 // ---------------------------------------------------------------------------------------
-template <typename T, bool SYNTH, bool STAGE>
+template <typename T, bool SYNTH, bool LDSMAP>
 __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Xchg<T> xs[2];
@@ -232,9 +232,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
     reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
   const Consts<T>& c = cs;
-  // LDS: [map blob][route tables if STAGE]
-  const Map<T> map = stage_map(a, smem);
-  unsigned char* route_lds = smem + ((a.map_bytes + 255) & ~255);
+  // LDS: the map blob (edges, index, classes).  Route tables stay in HBM (Route caches the
+  // active leg); keeping the block under 64 KB of LDS matters: a larger allocation measured
+  // ~1.75x slower at the same occupancy-limited grid.
+  const Map<T> map = LDSMAP ? stage_map(a, smem) : a.map;
   const int lane = threadIdx.x & (kWave - 1);
   const int type = threadIdx.x >> 6;             // wave-uniform
   const int n_env = a.n_env;
@@ -259,19 +260,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     rt.end_n = a.sc.end_n[sid];
     rt.end_e = a.sc.end_e[sid];
     v_des = init_val(a.sc, type, SIT_INIT_DESIRED_SPEED, env, n_env);
-    T* gn = a.st.wn + (size_t)type * a.cap * n_env + env;
-    T* ge = a.st.we + (size_t)type * a.cap * n_env + env;
-    if (STAGE) {
-      T* ln = reinterpret_cast<T*>(route_lds) + (size_t)type * a.cap * kWave + lane;
-      T* le = ln + (size_t)2 * a.cap * kWave;
-      for (int i = 0; i < rt.nw - 1; ++i) {
-        ln[i * kWave] = gn[(size_t)i * n_env];
-        le[i * kWave] = ge[(size_t)i * n_env];
-      }
-      rt.tn = ln; rt.te = le; rt.stride = kWave;
-    } else {
-      rt.tn = gn; rt.te = ge; rt.stride = n_env;
-    }
+    rt.tn = a.st.wn + (size_t)type * a.cap * n_env + env;
+    rt.te = a.st.we + (size_t)type * a.cap * n_env + env;
+    rt.stride = n_env;
+    rt.load_leg(s.k);
     if (type == 1) {
       samp = a.st.env[0][env]; eps = a.st.env[1][env];
       ppn = a.st.env[2][env]; ppe = a.st.env[3][env];
@@ -319,14 +311,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           o_rpm = s.lrpm; o_ect = s.lect; o_pme = s.lpme;
         } else {
           if (sac) {                     // update_route: insert at index -1 (Q16)
-            if (rt.nw < a.cap) {
-              const int i = rt.nw - 1;
-              rt.tn[i * rt.stride] = iwn;
-              rt.te[i * rt.stride] = iwe;
-              rt.nw += 1;
-            } else {
-              bits |= SIT_ST_ROUTE_OVERFLOW;
-            }
+            if (!rt.insert(iwn, iwe, s.k, a.cap)) bits |= SIT_ST_ROUTE_OVERFLOW;
             samp = T(0);
           }
           const T pre_n = s.n, pre_e = s.e;
@@ -361,8 +346,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       }
 
       // ---------------- own termination predicates (MSRL_env_ex.py:628-881) ----------------
-#ifdef SIT_ABLATE_PREDICATES   // diagnostic builds only (tools/ablate.sh): polygon work removed
+#if defined(SIT_ABLATE_PREDICATES)   // diagnostic builds only (tools/ablate.sh): polygon work removed
       const T dobst = T(1000);
+      const bool terrain = false;
+#elif defined(SIT_ABLATE_HULL)        // diagnostic: distance kept, hull test removed
+      const T dobst = distance_indexed(c, map, s.n, s.e);
       const bool terrain = false;
 #else
       const T dobst = distance_indexed(c, map, s.n, s.e);
@@ -398,7 +386,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           done = true;
           bits |= SIT_ST_OBS_TERRAIN;
         }
-#ifdef SIT_ABLATE_PREDICATES
+#if defined(SIT_ABLATE_PREDICATES) || defined(SIT_ABLATE_HULL)
         if (outside(c, iwn, iwe, T(0))) {
 #else
         if (outside(c, iwn, iwe, T(0)) || pip_point(c, map, iwn, iwe)) {   // Q11
@@ -487,6 +475,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       ep_step += 1;
       if (a.io.auto_reset && env_done) {
         reset_ship(a.sc, type, env, n_env, s, rt.nw);
+        rt.load_leg(s.k);
         ep_step = 0;
         if (type == 1) { samp = T(0); eps = T(0); ++episodes; }
         for (int j = 0; j < lo_n; ++j) lo[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + lo_base + j];
@@ -499,14 +488,6 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   if (act) {
     store_ship(a.st, sid, s);
     a.st.nw[sid] = rt.nw;
-    if (STAGE) {
-      T* gn = a.st.wn + (size_t)type * a.cap * n_env + env;
-      T* ge = a.st.we + (size_t)type * a.cap * n_env + env;
-      for (int i = 0; i < rt.nw - 1; ++i) {
-        gn[(size_t)i * n_env] = rt.tn[i * kWave];
-        ge[(size_t)i * n_env] = rt.te[i * kWave];
-      }
-    }
     for (int j = 0; j < lo_n; ++j) a.st.last_obs[(size_t)(lo_base + j) * n_env + env] = lo[j];
     if (type == 1) {
       a.st.env[0][env] = samp; a.st.env[1][env] = eps;
@@ -536,6 +517,7 @@ __global__ __launch_bounds__(256) void k_init_step(const KArgs<T> a, const uint8
   rt.tn = a.st.wn + (size_t)type * a.cap * n_env + env;
   rt.te = a.st.we + (size_t)type * a.cap * n_env + env;
   rt.stride = n_env;
+  rt.load_leg(s.k);
   init_step_ship(a.c, s, rt, init_val(a.sc, type, SIT_INIT_DESIRED_SPEED, env, n_env));
   store_ship(a.st, sid, s);
 }
@@ -616,10 +598,11 @@ struct sit_handle {
   // map
   unsigned char* map = nullptr;
   int n_poly = 0, n_vert = 0;
-  size_t map_idx = 0, map_off = 0, map_bbox = 0;
+  size_t map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0;
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
+  double fx0 = 0, fy0 = 0, finvx = 0, finvy = 0;
   double min_n = 0, max_n = 0, min_e = 0, max_e = 0;
   bool have_map = false, have_routes = false, have_init = false;
 };
@@ -736,6 +719,7 @@ Consts<T> make_consts(const sit_handle* h) {
   c.gx0 = (T)h->gx0; c.gy0 = (T)h->gy0; c.ginvx = (T)h->ginvx; c.ginvy = (T)h->ginvy;
   c.by0 = (T)h->by0; c.binv = (T)h->binv;
   c.hull_safe = (T)(l / 2 * std::sqrt(2.0) + 1.0);
+  c.fx0 = (T)h->fx0; c.fy0 = (T)h->fy0; c.finvx = (T)h->finvx; c.finvy = (T)h->finvy;
   return c;
 }
 
@@ -767,6 +751,7 @@ KArgs<T> make_args(const sit_handle* h) {
   a.map.use_index = h->use_index;
   a.map.edge = reinterpret_cast<const Edge<T>*>(h->map);
   a.map.idx = reinterpret_cast<const uint16_t*>(h->map + h->map_idx);
+  a.map.fine = reinterpret_cast<const uint32_t*>(h->map + h->map_fine);
   a.map.off = reinterpret_cast<const int32_t*>(h->map + h->map_off);
   a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
   a.map_bytes = (int32_t)h->map_bytes;
@@ -781,8 +766,8 @@ int ready(sit_handle* h) {
   return SIT_OK;
 }
 
-template <typename T>
-size_t route_lds_bytes(const sit_handle* h) { return (size_t)2 * 2 * h->cap * kWave * sizeof(T); }
+// LDS budget of one step-kernel block: above 64 KB a block measured ~1.75x slower
+constexpr size_t kLdsBudget = 64 * 1024;
 size_t map_lds_bytes(const sit_handle* h) { return (h->map_bytes + 255) & ~size_t(255); }
 
 template <typename T>
@@ -791,22 +776,23 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   a.io = io;
   const int blocks = (h->n_env + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const bool synth = io.action_ne == nullptr;
-  const size_t rlds = route_lds_bytes<T>(h);
-  const bool stage = io.n_steps > 1 && rlds + map_lds_bytes(h) <= 112 * 1024;
-  const size_t lds = map_lds_bytes(h) + (stage ? rlds : 0);
-  {
-    const void* fn = synth ? (stage ? (const void*)k_env_steps<T, true, true> : (const void*)k_env_steps<T, true, false>)
-                           : (stage ? (const void*)k_env_steps<T, false, true> : (const void*)k_env_steps<T, false, false>);
+  // the map (edges, index, classes) is staged in LDS when it fits the budget next to the
+  // static exchange buffers; otherwise the predicates read it through the caches
+  const size_t stat = sizeof(Xchg<T>) * 2 + sizeof(Consts<T>) + 256;
+  const bool lds_map = map_lds_bytes(h) + stat <= kLdsBudget;
+  const size_t lds = lds_map ? map_lds_bytes(h) : 0;
+  if (lds_map) {
+    const void* fn = synth ? (const void*)k_env_steps<T, true, true> : (const void*)k_env_steps<T, false, true>;
     HIP_TRY(h, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   }
-  if (synth && stage)
+  if (synth && lds_map)
     hipLaunchKernelGGL((k_env_steps<T, true, true>), dim3(blocks), dim3(128), lds, stream, a);
   else if (synth)
-    hipLaunchKernelGGL((k_env_steps<T, true, false>), dim3(blocks), dim3(128), lds, stream, a);
-  else if (stage)
+    hipLaunchKernelGGL((k_env_steps<T, true, false>), dim3(blocks), dim3(128), 0, stream, a);
+  else if (lds_map)
     hipLaunchKernelGGL((k_env_steps<T, false, true>), dim3(blocks), dim3(128), lds, stream, a);
   else
-    hipLaunchKernelGGL((k_env_steps<T, false, false>), dim3(blocks), dim3(128), lds, stream, a);
+    hipLaunchKernelGGL((k_env_steps<T, false, false>), dim3(blocks), dim3(128), 0, stream, a);
   HIP_TRY(h, hipGetLastError());
   return SIT_OK;
 }
@@ -1018,9 +1004,8 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
       if (std::min(vy[e], byv[e]) <= hi && std::max(vy[e], byv[e]) >= lo) bentries.push_back((uint16_t)e);
   }
   bstart[kBands] = (uint32_t)bentries.size();
-  // cell classes: pure cells (no boundary within 1 m of the cell) take the side of their centre
-  std::vector<uint16_t> cls(kGrid * kGrid, 2);
-  auto inside_center = [&](double px, double py) {   // crossing number; the point is >= 1 m off every edge
+  // point-in-polygon by crossing number for class-grid cell centres (>= 1 m off every edge)
+  auto inside_center = [&](double px, double py) {
     bool in = false;
     for (int p = 0; p < n_poly; ++p) {
       int cross = 0;
@@ -1035,14 +1020,22 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     }
     return in;
   };
-  for (int j = 0; j < kGrid; ++j)
-    for (int i = 0; i < kGrid; ++i) {
-      const double cx = gx0 + (i + 0.5) * sx, cy = gy0 + (j + 0.5) * sy;
+  // fine 2-bit classes over the map extent + 100 m
+  const double fx0 = h->min_e - 100.0, fy0 = h->min_n - 100.0;
+  const double fsx = (ext_x + 200.0) / kFine, fsy = (ext_y + 200.0) / kFine;
+  const double fhd = 0.5 * std::sqrt(fsx * fsx + fsy * fsy) + 1.0;
+  std::vector<uint32_t> fine(kFineWords, 0);
+  for (int j = 0; j < kFine; ++j)
+    for (int i = 0; i < kFine; ++i) {
+      const double cx = fx0 + (i + 0.5) * fsx, cy = fy0 + (j + 0.5) * fsy;
       double dmin = INFINITY;
-      for (int e = 0; e < nv; ++e) dmin = std::min(dmin, seg_dist(cx, cy, e));
-      if (dmin > hd + 1.0) cls[j * kGrid + i] = inside_center(cx, cy) ? 1 : 0;
+      for (int e = 0; e < nv && dmin > fhd + 1.0; ++e) dmin = std::min(dmin, seg_dist(cx, cy, e));
+      const uint32_t k = dmin > fhd + 1.0 ? (inside_center(cx, cy) ? 1u : 0u) : 2u;
+      const int cell = j * kFine + i;
+      fine[cell >> 4] |= k << ((cell & 15) * 2);
     }
-  const size_t head = (size_t)kClassBase + kGrid * kGrid;
+  h->fx0 = fx0; h->fy0 = fy0; h->finvx = 1.0 / fsx; h->finvy = 1.0 / fsy;
+  const size_t head = (size_t)kIdxHead;
   const size_t n_idx = head + gentries.size() + bentries.size();
   h->use_index = (n_idx < 65535 && n_idx * 2 <= 48 * 1024) ? 1 : 0;
   h->gx0 = gx0; h->gy0 = gy0; h->ginvx = 1.0 / sx; h->ginvy = 1.0 / sy;
@@ -1051,14 +1044,14 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
   if (h->use_index) {
     for (int c = 0; c <= kGrid * kGrid; ++c) idx[c] = (uint16_t)(head + gstart[c]);
     for (int b = 0; b <= kBands; ++b) idx[kBandBase + b] = (uint16_t)(head + gentries.size() + bstart[b]);
-    std::copy(cls.begin(), cls.end(), idx.begin() + kClassBase);
     std::copy(gentries.begin(), gentries.end(), idx.begin() + head);
     std::copy(bentries.begin(), bentries.end(), idx.begin() + head + gentries.size());
   }
-  // blob: [Edge<T>[nv]][u16 index] (staged into LDS) [ring offsets][bboxes] (fallback, global)
+  // blob: [Edge<T>[nv]][u16 index][u32 classes] (staged into LDS) [ring offsets][bboxes] (fallback, global)
   const size_t esz = rs == 8 ? sizeof(Edge<double>) : sizeof(Edge<float>);
   size_t o = align256(nv * esz);
   h->map_idx = o; o = align256(o + idx.size() * 2);
+  h->map_fine = o; o = align256(o + fine.size() * 4);
   h->map_bytes = o;
   h->map_off = o; o = align256(o + (n_poly + 1) * 4);
   h->map_bbox = o; o = align256(o + 4 * n_poly * rs);
@@ -1073,6 +1066,7 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     }
   }
   std::memcpy(host.data() + h->map_idx, idx.data(), idx.size() * 2);
+  std::memcpy(host.data() + h->map_fine, fine.data(), fine.size() * 4);
   std::memcpy(host.data() + h->map_off, offs.data(), (n_poly + 1) * 4);
   for (size_t i = 0; i < bbox.size(); ++i) {
     if (rs == 8) reinterpret_cast<double*>(host.data() + h->map_bbox)[i] = bbox[i];
