@@ -221,6 +221,69 @@ struct Xchg {
 // the env step kernel: K steps of MultiShipRLEnv.step (+ optional auto-reset)
 //   SYNTH : actions from the synthetic AST sampler (else explicit arrays)
 // ---------------------------------------------------------------------------------------
+#ifdef SIT_DIAG_PATHS
+// Diagnostic builds only (tools/diag_paths.py): per-wave path statistics of the predicates.
+// Counter layout per ship type: see tools/diag_paths.py.
+__device__ unsigned long long g_sit_diag[2][16];
+
+template <typename T>
+__device__ int diag_band_len(const Consts<T>& c, const Map<T>& m, T n) {
+  const T fb = (n - c.by0) * c.binv;
+  if (!m.use_index || !(fb >= T(0) && fb < T(kBands))) return 0;
+  const int b = (int)fb;
+  return m.idx[kBandBase + b + 1] - m.idx[kBandBase + b];
+}
+
+template <typename T>
+__device__ void diag_lane(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst, bool iw, T iwn, T iwe,
+                          int* v) {
+  const T fx = (e - c.gx0) * c.ginvx, fy = (n - c.gy0) * c.ginvy;
+  if (m.use_index && fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)) {
+    const int cell = (int)fy * kGrid + (int)fx;
+    v[0] = m.idx[cell + 1] - m.idx[cell];
+  }
+  if (dobst <= c.hull_safe) {
+    v[1] = 1;
+    const T h = c.half_len;
+    const int c00 = fine_class(c, m, n - h, e - h), c01 = fine_class(c, m, n - h, e + h);
+    const int c10 = fine_class(c, m, n + h, e - h), c11 = fine_class(c, m, n + h, e + h);
+    if (!(c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1)) {
+      if (c00 >= 2 || c01 >= 2) { v[2] += 1; v[3] += diag_band_len(c, m, n - h); }
+      if (c10 >= 2 || c11 >= 2) { v[2] += 1; v[3] += diag_band_len(c, m, n + h); }
+    }
+  } else if (fine_class(c, m, n, e) >= 2) {
+    v[4] = 1;
+    v[3] += diag_band_len(c, m, n);
+  }
+  if (iw && fine_class(c, m, iwn, iwe) >= 2) { v[5] = 1; v[6] = diag_band_len(c, m, iwn); }
+}
+
+__device__ void diag_wave(int type, int lane, bool act, const int* v) {
+  // lane sums and wave maxima / any-counts (the wave pays the max over its lanes)
+  unsigned long long* g = g_sit_diag[type];
+  int mx[7], any[7];
+  for (int j = 0; j < 7; ++j) {
+    int m = act ? v[j] : 0;
+    for (int off = 32; off >= 1; off >>= 1) m = max(m, __shfl_xor(m, off));
+    mx[j] = m;
+    any[j] = __popcll(__ballot(act && v[j] != 0));
+  }
+  if (act) {
+    for (int j = 0; j < 7; ++j) if (v[j]) atomicAdd(&g[j], (unsigned long long)v[j]);
+  }
+  if (lane == 0) {
+    atomicAdd(&g[7], 1ull);
+    atomicAdd(&g[8], (unsigned long long)mx[0]);            // max distance candidates
+    atomicAdd(&g[9], (unsigned long long)(any[1] > 0));     // waves with a near-shore lane
+    atomicAdd(&g[10], (unsigned long long)(any[2] > 0));    // waves with a pair scan
+    atomicAdd(&g[11], (unsigned long long)mx[3]);           // max hull band trips
+    atomicAdd(&g[12], (unsigned long long)(any[4] > 0));    // waves with a mixed far centre
+    atomicAdd(&g[13], (unsigned long long)(any[5] > 0));    // waves with a mixed IW
+    atomicAdd(&g[14], (unsigned long long)mx[6]);           // max IW band trips
+  }
+}
+#endif
+
 template <typename T, bool SYNTH, bool LDSMAP>
 __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -247,6 +310,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   Route<T> rt{};
   T v_des = T(0);
   T samp = T(0), eps = T(0), ppn = T(0), ppe = T(0), iwn = T(0), iwe = T(0);
+  // the IW's terrain test is a pure function of (iwn, iwe), which change only at sampling
+  // events (or with the caller's action): cache it
+  T iw_tn = T(0), iw_te = T(0);
+  bool iw_valid = false, iw_in = false;
   int ep_step = 0;
   uint32_t event = 0, episodes = 0;
   double ab_len = 0.0, ab_alpha = 0.0;
@@ -284,6 +351,9 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     T o_rpm = T(0), o_ect = T(0), o_pme = T(0);
     T r_nt = T(0), r_term = T(0);
     uint32_t bits = 0;
+#ifdef SIT_DIAG_PATHS
+    int dv[7] = {0, 0, 0, 0, 0, 0, 0};
+#endif
     bool sac = false, init_f = false;
     double ang = NAN;
     if (act) {
@@ -356,6 +426,9 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       const T dobst = distance_indexed(c, map, s.n, s.e);
       const bool terrain = hull_in_terrain(c, map, s.n, s.e, dobst);
 #endif
+#ifdef SIT_DIAG_PATHS
+      diag_lane(c, map, s.n, s.e, dobst, type == 1, iwn, iwe, dv);
+#endif
       const T dn_end = s.n - rt.end_n, de_end = s.e - rt.end_e;
       const bool arrive = xsqrt(dn_end * dn_end + de_end * de_end) <= c.arrival_radius;
       const bool horizon = outside(c, s.n, s.e, c.half_len);
@@ -389,7 +462,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #if defined(SIT_ABLATE_PREDICATES) || defined(SIT_ABLATE_HULL)
         if (outside(c, iwn, iwe, T(0))) {
 #else
-        if (outside(c, iwn, iwe, T(0)) || pip_point(c, map, iwn, iwe)) {   // Q11
+        if (!iw_valid || iwn != iw_tn || iwe != iw_te) {
+          iw_in = pip_point(c, map, iwn, iwe);
+          iw_tn = iwn; iw_te = iwe; iw_valid = true;
+        }
+        if (outside(c, iwn, iwe, T(0)) || iw_in) {   // Q11
 #endif
           if (!stop) r_term = r_term - T(1000);
           stop = 1; done = true;
@@ -414,6 +491,9 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       if (type == 1) { x.r_nto[lane] = r_nt; x.r_o[lane] = r_term; }
     }
     __syncthreads();
+#ifdef SIT_DIAG_PATHS
+    diag_wave(type, lane, act, dv);
+#endif
     // ---------------- env level: shared reward, outputs ----------------
     bool env_done = false;
     if (act) {
@@ -803,6 +883,18 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
 // C ABI
 // =======================================================================================
 extern "C" {
+
+#ifdef SIT_DIAG_PATHS
+int sit_diag_read(unsigned long long* out, int reset) {   // diagnostic builds only
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sit_diag), sizeof(g_sit_diag)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[2][16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sit_diag), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 int32_t sit_abi_version(void) { return SIT_ABI_VERSION; }
 size_t sit_params_size(void) { return sizeof(sit_params); }
