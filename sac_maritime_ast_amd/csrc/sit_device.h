@@ -83,12 +83,15 @@ struct Consts {
 // LDS base pointer, immediate field offsets) so the predicates need no per-array registers.
 //
 // Spatial index (built on the host by sit_load_map, exact by construction), one u16 array:
-//   idx[0 .. G*G]            grid cell starts (absolute positions in idx)
-//   idx[G*G+1 .. G*G+1+NB]   band starts
-//   then the entries (edge ids).
+//   idx[0 .. 2*G*G)          grid cell records, one u32 each: first group (in 4-id groups
+//                            from the start of idx) | group count << 16
+//   idx[kBandBase ..]        NB+1 band starts (absolute positions in idx)
+//   then the band entries (edge ids), then the grid groups (8-byte aligned).
 //  * grid: G x G cells over the map extent plus a margin; cell c lists every edge that can be
 //    the nearest edge of some point within 1 m of the cell (conservative bound with a 1 m
-//    float slack), so the minimum over the list equals the minimum over all edges.
+//    float slack), so the minimum over the list equals the minimum over all edges.  A list is
+//    padded to a multiple of 4 with its first id, so one 8-byte LDS read yields 4 ids whose
+//    edge loads are independent (duplicates do not change a minimum).
 //  * bands: NB horizontal bands; band b lists every edge whose y-range meets the band (+-1 m).
 //    GEOS's ray-crossing test only looks at edges whose y-range contains the point's y.
 //  * classes (separate u32 array): kFine x kFine cells over the map extent + 100 m, 2 bits per
@@ -98,7 +101,7 @@ struct Consts {
 //    ~31 m from the shore resolves by one lookup.
 constexpr int kGrid = 32;
 constexpr int kBands = 64;
-constexpr int kBandBase = kGrid * kGrid + 1;
+constexpr int kBandBase = 2 * kGrid * kGrid;
 constexpr int kIdxHead = kBandBase + kBands + 1;
 constexpr int kFine = 256;
 constexpr int kFineWords = kFine * kFine / 16;
@@ -385,7 +388,10 @@ __device__ __forceinline__ T edge_dist2(const Edge<T>& g, T px, T py) {
   const T rx = px - g.bx, ry = py - g.by;
   const T cr = qy * ex - qx * ey;
   const T d_a = qx * qx + qy * qy, d_b = rx * rx + ry * ry, d_s = cr * cr * g.il2;
-  return (g.il2 == T(0) || t <= T(0)) ? d_a : (t * g.il2 >= T(1) ? d_b : d_s);
+  // branch-free selection (all three are cheap): keeps the edge loads of a candidate group
+  // independent, so they issue back to back instead of one LDS round trip per candidate
+  const T d_bs = (t * g.il2 >= T(1)) ? d_b : d_s;
+  return ((g.il2 == T(0)) | (t <= T(0))) ? d_a : d_bs;
 }
 
 // min over polygons of exterior.distance(Point(e, n)), full scan
@@ -403,10 +409,19 @@ __device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   if (!m.use_index || !(fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)))
     return distance_to_polys(m, n, e);
   const int cell = (int)fy * kGrid + (int)fx;
-  const int k0 = m.idx[cell], k1 = m.idx[cell + 1];
+  const uint32_t rec = reinterpret_cast<const uint32_t*>(m.idx)[cell];
+  const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (rec & 0xffffu);
+  const int ng = (int)(rec >> 16);
   T best = T(3.0e38);
 #pragma unroll 1
-  for (int k = k0; k < k1; ++k) best = xmin(best, edge_dist2(m.edge[m.idx[k]], e, n));
+  for (int g = 0; g < ng; ++g) {
+    const uint2 q = grp[g];
+    const T d0 = edge_dist2(m.edge[q.x & 0xffffu], e, n);
+    const T d1 = edge_dist2(m.edge[q.x >> 16], e, n);
+    const T d2 = edge_dist2(m.edge[q.y & 0xffffu], e, n);
+    const T d3 = edge_dist2(m.edge[q.y >> 16], e, n);
+    best = xmin(best, xmin(xmin(d0, d1), xmin(d2, d3)));
+  }
   return xsqrt(best);
 }
 

@@ -221,10 +221,27 @@ struct Xchg {
 // the env step kernel: K steps of MultiShipRLEnv.step (+ optional auto-reset)
 //   SYNTH : actions from the synthetic AST sampler (else explicit arrays)
 // ---------------------------------------------------------------------------------------
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
+// Diagnostic builds only (tools/diag_paths.py): [type][0..15] predicate path statistics,
+// [type][16..23] shader-clock cycles per step phase (wave lane 0).
+__device__ unsigned long long g_sit_diag[2][32];
+#endif
+#ifdef SIT_DIAG_PHASES
+// the fence makes the ship state live in registers at the timer, so arithmetic cannot be
+// sunk across a phase boundary
+template <typename T>
+__device__ __forceinline__ void diag_fence(Ship<T>& s) {
+  asm volatile("" : "+v"(s.n), "+v"(s.e), "+v"(s.psi), "+v"(s.u), "+v"(s.v), "+v"(s.r), "+v"(s.w),
+                    "+v"(s.i1), "+v"(s.i2), "+v"(s.hi), "+v"(s.hp), "+v"(s.ect_int));
+  asm volatile("" : "+v"(s.lrpm), "+v"(s.lect), "+v"(s.lpme), "+v"(s.k), "+v"(s.ticks), "+v"(s.stop));
+}
+#define SIT_PH(k) do { diag_fence(s); __builtin_amdgcn_sched_barrier(0); \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph[k] += t_ - ph_t; ph_t = t_; \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define SIT_PH(k) do { } while (0)
+#endif
 #ifdef SIT_DIAG_PATHS
-// Diagnostic builds only (tools/diag_paths.py): per-wave path statistics of the predicates.
-// Counter layout per ship type: see tools/diag_paths.py.
-__device__ unsigned long long g_sit_diag[2][16];
 
 template <typename T>
 __device__ int diag_band_len(const Consts<T>& c, const Map<T>& m, T n) {
@@ -240,7 +257,7 @@ __device__ void diag_lane(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst
   const T fx = (e - c.gx0) * c.ginvx, fy = (n - c.gy0) * c.ginvy;
   if (m.use_index && fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)) {
     const int cell = (int)fy * kGrid + (int)fx;
-    v[0] = m.idx[cell + 1] - m.idx[cell];
+    v[0] = (int)(reinterpret_cast<const uint32_t*>(m.idx)[cell] >> 16) * 4;
   }
   if (dobst <= c.hull_safe) {
     v[1] = 1;
@@ -343,6 +360,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   }
   const T maxn = c.max_n;
   __syncthreads();   // map staged
+#ifdef SIT_DIAG_PHASES
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ph_t = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int step = 0; step < a.io.n_steps; ++step) {
     const size_t row = (size_t)step * n_env + env;
@@ -423,8 +444,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       const T dobst = distance_indexed(c, map, s.n, s.e);
       const bool terrain = false;
 #else
+      SIT_PH(0);
       const T dobst = distance_indexed(c, map, s.n, s.e);
+      SIT_PH(1);
       const bool terrain = hull_in_terrain(c, map, s.n, s.e, dobst);
+      SIT_PH(2);
 #endif
 #ifdef SIT_DIAG_PATHS
       diag_lane(c, map, s.n, s.e, dobst, type == 1, iwn, iwe, dv);
@@ -490,7 +514,9 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       x.bits[type][lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u);
       if (type == 1) { x.r_nto[lane] = r_nt; x.r_o[lane] = r_term; }
     }
+    SIT_PH(3);
     __syncthreads();
+    SIT_PH(4);
 #ifdef SIT_DIAG_PATHS
     diag_wave(type, lane, act, dv);
 #endif
@@ -550,6 +576,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       const unsigned long long m = __ballot(env_done);
       if (lane == 0 && m) atomicAdd(a.io.done_count + step, (int)__popcll(m));
     }
+    SIT_PH(5);
     // ---------------- auto reset: reset() + init_step() (test_beds/main_ast.py:314-329) ----------------
     if (act) {
       ep_step += 1;
@@ -562,7 +589,12 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         init_step_ship(c, s, rt, v_des);
       }
     }
+    SIT_PH(6);
   }
+#ifdef SIT_DIAG_PHASES
+  if (lane == 0)
+    for (int k = 0; k < 7; ++k) atomicAdd(&g_sit_diag[type][16 + k], ph[k]);
+#endif
 
   // ---------------- write back ----------------
   if (act) {
@@ -884,12 +916,12 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
 // =======================================================================================
 extern "C" {
 
-#ifdef SIT_DIAG_PATHS
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
 int sit_diag_read(unsigned long long* out, int reset) {   // diagnostic builds only
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sit_diag), sizeof(g_sit_diag)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[2][16] = {};
+    unsigned long long z[2][32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_sit_diag), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;
@@ -1074,7 +1106,7 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     t = std::min(1.0, std::max(0.0, t));
     return std::hypot(px - (vx[i] + t * ex), py - (vy[i] + t * ey));
   };
-  // packed u16 index: [grid starts (G*G+1)][band starts (NB+1)][entries]
+  // packed u16 index: [grid records (u32 per cell)][band starts (NB+1)][band entries][grid groups]
   std::vector<uint16_t> gentries, bentries;
   std::vector<uint32_t> gstart(kGrid * kGrid + 1), bstart(kBands + 1);
   std::vector<double> dcell(nv);
@@ -1084,8 +1116,10 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
       double D = INFINITY;
       for (int e = 0; e < nv; ++e) { dcell[e] = seg_dist(cx, cy, e); D = std::min(D, dcell[e] + hd); }
       gstart[j * kGrid + i] = (uint32_t)gentries.size();
+      const size_t first = gentries.size();
       for (int e = 0; e < nv; ++e)
         if (dcell[e] - hd <= D + 1.0) gentries.push_back((uint16_t)e);
+      while ((gentries.size() - first) % 4) gentries.push_back(gentries[first]);
     }
   gstart[kGrid * kGrid] = (uint32_t)gentries.size();
   const double by0 = h->min_n - 1.0, bh = (ext_y + 2.0) / kBands;
@@ -1128,16 +1162,20 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     }
   h->fx0 = fx0; h->fy0 = fy0; h->finvx = 1.0 / fsx; h->finvy = 1.0 / fsy;
   const size_t head = (size_t)kIdxHead;
-  const size_t n_idx = head + gentries.size() + bentries.size();
+  const size_t gbase = (head + bentries.size() + 3) & ~size_t(3);   // 8-byte aligned groups
+  const size_t n_idx = gbase + gentries.size();
   h->use_index = (n_idx < 65535 && n_idx * 2 <= 48 * 1024) ? 1 : 0;
   h->gx0 = gx0; h->gy0 = gy0; h->ginvx = 1.0 / sx; h->ginvy = 1.0 / sy;
   h->by0 = by0; h->binv = 1.0 / bh;
   std::vector<uint16_t> idx(h->use_index ? n_idx : 2, 0);
   if (h->use_index) {
-    for (int c = 0; c <= kGrid * kGrid; ++c) idx[c] = (uint16_t)(head + gstart[c]);
-    for (int b = 0; b <= kBands; ++b) idx[kBandBase + b] = (uint16_t)(head + gentries.size() + bstart[b]);
-    std::copy(gentries.begin(), gentries.end(), idx.begin() + head);
-    std::copy(bentries.begin(), bentries.end(), idx.begin() + head + gentries.size());
+    for (int c = 0; c < kGrid * kGrid; ++c) {
+      idx[2 * c] = (uint16_t)((gbase + gstart[c]) / 4);             // first group
+      idx[2 * c + 1] = (uint16_t)((gstart[c + 1] - gstart[c]) / 4); // group count
+    }
+    for (int b = 0; b <= kBands; ++b) idx[kBandBase + b] = (uint16_t)(head + bstart[b]);
+    std::copy(bentries.begin(), bentries.end(), idx.begin() + head);
+    std::copy(gentries.begin(), gentries.end(), idx.begin() + gbase);
   }
   // blob: [Edge<T>[nv]][u16 index][u32 classes] (staged into LDS) [ring offsets][bboxes] (fallback, global)
   const size_t esz = rs == 8 ? sizeof(Edge<double>) : sizeof(Edge<float>);
