@@ -227,7 +227,8 @@ int sit_init_step(sit_handle* h, const uint8_t* env_mask, void* stream);
  *   sac_update u8[n_env]       SAC_update: insert the IW into the obstacle ship's route
  *   init       u8[n_env]       init: first step of an episode (no distance accounting)
  *   next_state real[n_env][SIT_OBS_DIM], reward real[n_env], done u8[n_env], status u32[n_env]
- *   done_count int32[1] or NULL: += number of envs with done (wave ballot reduction) */
+ *   done_count int32[1] or NULL: += number of envs with done (wave ballot reduction)
+ * next_state (and action_out below) must be aligned to 2 reals (SIT_E_INVALID otherwise). */
 int sit_step(sit_handle* h, const void* action_ne, const uint8_t* sac_update,
              const uint8_t* init, void* next_state, void* reward, uint8_t* done,
              uint32_t* status, int32_t* done_count, void* stream);

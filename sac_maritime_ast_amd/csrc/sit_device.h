@@ -14,7 +14,12 @@
 namespace sit {
 
 constexpr int kWave = 64;         // CDNA wavefront
-constexpr int kEnvsPerBlock = 64; // one wave of test ships + one wave of obstacle ships
+#ifndef SIT_ENVS_PER_BLOCK
+#define SIT_ENVS_PER_BLOCK 64
+#endif
+// envs per step-kernel block: one wave of test ships + one wave of obstacle ships, the first
+// kEnvsPerBlock lanes of each wave active
+constexpr int kEnvsPerBlock = SIT_ENVS_PER_BLOCK;
 constexpr int kMaxPolyVerts = 256;
 constexpr int kMaxPolys = 32;
 

@@ -301,17 +301,26 @@ __device__ void diag_wave(int type, int lane, bool act, const int* v) {
 }
 #endif
 
+// paired output stores: a state row (SIT_OBS_DIM reals) starts 8-byte (float) / 16-byte
+// (double) aligned, so pairs at even offsets go out as one 2-element store (fewer store
+// instructions per wave; the scattered row stride makes store issue, not bytes, the cost)
+__device__ __forceinline__ void store2(float* p, float a, float b) { *reinterpret_cast<float2*>(p) = make_float2(a, b); }
+__device__ __forceinline__ void store2(double* p, double a, double b) { *reinterpret_cast<double2*>(p) = make_double2(a, b); }
+
 template <typename T, bool SYNTH, bool LDSMAP>
 __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Xchg<T> xs[2];
-  // The ~70 per-step constants are read from a block copy in LDS: loads from LDS land in
-  // VGPRs (one wave per SIMD leaves plenty), whereas kernel-argument constants compete for
-  // the 102 SGPRs and spill to VGPR lanes (v_readlane in the loop).
+  // The ~70 per-step constants go kernel arguments -> LDS -> VGPRs: loaded through LDS they
+  // land in vector registers (one wave per SIMD leaves ~512 per lane, AGPRs included), whereas
+  // kernel-argument constants compete for the 102 SGPRs and spill to VGPR lanes (v_readlane
+  // in the loop), and reading the LDS block inside the loop put ~40 dependent LDS reads on
+  // each step's critical path (the register copy measured 12% faster).
   __shared__ Consts<T> cs;
   for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
     reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
-  const Consts<T>& c = cs;
+  __syncthreads();
+  const Consts<T> c = cs;
   // LDS: the map blob (edges, index, classes).  Route tables stay in HBM (Route caches the
   // active leg); keeping the block under 64 KB of LDS matters: a larger allocation measured
   // ~1.75x slower at the same occupancy-limited grid.
@@ -320,7 +329,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   const int type = threadIdx.x >> 6;             // wave-uniform
   const int n_env = a.n_env;
   const int env = blockIdx.x * kEnvsPerBlock + lane;
-  const bool act = env < n_env;
+  const bool act = lane < kEnvsPerBlock && env < n_env;
   const int sid = type * n_env + env;
 
   Ship<T> s{};
@@ -547,16 +556,16 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         if (a.io.status) a.io.status[row] = status;
         if (a.io.next_state) {
           T* ns = a.io.next_state + row * SIT_OBS_DIM;
-          ns[0] = s.n; ns[1] = s.e; ns[2] = s.psi; ns[3] = o_rpm; ns[4] = o_ect; ns[5] = o_pme;
+          store2(ns, s.n, s.e); store2(ns + 2, s.psi, o_rpm); store2(ns + 4, o_ect, o_pme);
         }
       } else {
         if (a.io.next_state) {
           T* ns = a.io.next_state + row * SIT_OBS_DIM;
-          ns[6] = s.n; ns[7] = s.e; ns[8] = s.psi; ns[9] = o_ect;
+          store2(ns + 6, s.n, s.e); store2(ns + 8, s.psi, o_ect);
         }
         if (a.io.action_out) {
           T* ao = a.io.action_out + row * 4;
-          ao[0] = iwn; ao[1] = iwe; ao[2] = (T)ang; ao[3] = sac ? T(1) : T(0);
+          store2(ao, iwn, iwe); store2(ao + 2, (T)ang, sac ? T(1) : T(0));
         }
         const int slot = x.slot[lane];
         if (slot >= 0 && slot < a.io.transition_capacity) {
@@ -1330,6 +1339,12 @@ int sit_init_step(sit_handle* h, const uint8_t* env_mask, void* stream) {
   return SIT_OK;
 }
 
+// next_state and action_out rows are written with paired stores (store2)
+static bool pair_aligned(const sit_handle* h, const void* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  return (a % (2 * (h->precision == SIT_F64 ? sizeof(double) : sizeof(float)))) == 0;
+}
+
 int sit_step(sit_handle* h, const void* action_ne, const uint8_t* sac_update, const uint8_t* init,
              void* next_state, void* reward, uint8_t* done, uint32_t* status, int32_t* done_count,
              void* stream) {
@@ -1337,6 +1352,7 @@ int sit_step(sit_handle* h, const void* action_ne, const uint8_t* sac_update, co
   if (rc) return rc;
   if (!action_ne || !sac_update || !init) return fail(h, SIT_E_INVALID, "action_ne, sac_update and init are required");
   if (!next_state && !reward) return fail(h, SIT_E_INVALID, "need next_state or reward output");
+  if (!pair_aligned(h, next_state)) return fail(h, SIT_E_INVALID, "next_state must be aligned to 2 reals");
   if (h->precision == SIT_F64) {
     StepIO<double> io{};
     io.n_steps = 1; io.action_ne = (const double*)action_ne; io.sac_update = sac_update; io.init = init;
@@ -1360,6 +1376,8 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
   if (ra->action_ne && (!ra->sac_update || !ra->init))
     return fail(h, SIT_E_INVALID, "explicit actions need sac_update and init");
   if (ra->env_id_offset < 0) return fail(h, SIT_E_INVALID, "env_id_offset must be >= 0");
+  if (!pair_aligned(h, ra->next_state) || !pair_aligned(h, ra->action_out))
+    return fail(h, SIT_E_INVALID, "next_state and action_out must be aligned to 2 reals");
   if (ra->transitions && (!ra->transition_count || ra->transition_capacity <= 0))
     return fail(h, SIT_E_INVALID, "transitions need transition_count and a positive capacity");
   auto fill = [&](auto* io, auto* tag) {

@@ -20,7 +20,7 @@ from oracle import sit_oracle as so
 pytestmark = pytest.mark.gpu
 
 sit = pytest.importorskip("sac_maritime_ast_amd")
-from sac_maritime_ast_amd import VecMultiShipRLEnv, make_scenario, status_string  # noqa: E402
+from sac_maritime_ast_amd import VecMultiShipRLEnv, _lib, make_scenario, status_string  # noqa: E402
 from sac_maritime_ast_amd.config import params as sit_params  # noqa: E402
 from sac_maritime_ast_amd.scenario import Scenario  # noqa: E402
 
@@ -273,3 +273,23 @@ def test_f64_replay_transitions_vs_oracle():
         assert rel_err(got[:, cols], want[:, cols], np.r_[OBS_SCALE, OBS_SCALE]).max() <= TOL64
         assert rel_err(got[:, 10:12], want[:, 10:12], 1.0).max() <= TOL64
     assert total > 2 * n_env
+
+
+def test_misaligned_output_rejected():
+    """Rows are written with paired stores: a next_state pointer off the 2-real alignment is
+    refused with SIT_E_INVALID (and nothing is launched), an aligned one is accepted."""
+    n = 64
+    env = VecMultiShipRLEnv(scenario=make_scenario(n), precision=32, device=DEV)
+    env.reset()
+    env.init_step()
+    a = torch.zeros((n, 2), dtype=torch.float32, device=DEV)
+    flags = torch.zeros((n,), dtype=torch.uint8, device=DEV)
+    buf = torch.zeros((n * 10 + 1,), dtype=torch.float32, device=DEV)
+    rew = torch.zeros((n,), dtype=torch.float32, device=DEV)
+    with pytest.raises(_lib.SitError, match="aligned"):
+        env._call("sit_step", a.data_ptr(), flags.data_ptr(), flags.data_ptr(), buf.data_ptr() + 4,
+                  rew.data_ptr(), None, None, None, env._stream())
+    env._call("sit_step", a.data_ptr(), flags.data_ptr(), flags.data_ptr(), buf.data_ptr(),
+              rew.data_ptr(), None, None, None, env._stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(buf[:n * 10]).all()
