@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--launch-trace", action="store_true", help="print every launch's kernel ms to stderr")
     return ap.parse_args()
 
 
@@ -212,7 +213,10 @@ def main():
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    launch_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_ms = float(np.mean(launch_ms))
+    if args.launch_trace:
+        print("launch_ms " + " ".join(f"{x:.4f}" for x in launch_ms), file=sys.stderr)
 
     st = env.get_state()
     mean_nw_obs = float(st["n_wpt"][1].double().mean().item())

@@ -211,6 +211,20 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets,
 int sit_load_routes(sit_handle* h, const double* wpt_ne, const int32_t* n_wpt);
 /* Construction-time values: init[env][ship][SIT_INIT_NF]. */
 int sit_load_initial(sit_handle* h, const double* init);
+/* Spatial-index statistics of the loaded map (diagnostics; no reference counterpart):
+ * info[0] bytes of the map blob staged into LDS per step-kernel block, [1] mixed class cells
+ * with a point-in-polygon record, [2] live edge entries of those records, [3] nearest-edge
+ * grid and bands in use, [4] cell records in use, [5] LDS bytes per block for the map.
+ * Writes min(n, 6) values. */
+int sit_map_info(const sit_handle* h, int64_t* info, int32_t n);
+/* The step kernel's map predicates at arbitrary points (test/diagnostic entry; the reference
+ * counterparts are PolygonObstacle.obstacles_distance / Polygon.contains / is_pos_inside_obstacles,
+ * obstacle.py:126-141, MSRL_env_ex.py:490-515), through the same spatial index:
+ *   pts_ne real[n][2] (north, east); dist real[n] boundary distance; inside u8[n] point strictly
+ *   inside a polygon; hull u8[n] any hull corner (+-l/2) inside.  Device pointers; any output may
+ *   be NULL. */
+int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint8_t* inside,
+                  uint8_t* hull, void* stream);
 /* Put every env into its construction-time state (as if freshly built).  Unlike
  * sit_reset this also re-initialises the shaft speed and all controller integrators. */
 int sit_restart(sit_handle* h, void* stream);

@@ -125,6 +125,16 @@ struct Map {
   const uint32_t* fine;     // [kFineWords] 2-bit cell classes (LDS copy in the step kernel)
   int32_t n_edge;
   int32_t use_index;        // 0: full scans only
+  // point-in-polygon records of the mixed class cells (LDS copy in the step kernel):
+  //   frank[w]  number of mixed cells in class words [0, w)   (rank of a mixed cell)
+  //   crec[r]   (x) per-polygon crossing parity that every point of the cell collects from the
+  //             edges whose contribution is the same for the whole cell (checked with a 1 m
+  //             margin on the host), (y) first | count << 16 of the cell's live edges in clive
+  //   clive[]   edge ids (u8) whose contribution varies inside the cell
+  const uint16_t* frank;
+  const uint2* crec;
+  const uint8_t* clive;
+  int32_t use_cells;
   // fallback scan (global memory): polygon ring offsets and bounding boxes
   const int32_t* off;       // [n_poly + 1]
   const T* bbox;            // [n_poly][4] min_x, max_x, min_y, max_y
@@ -465,20 +475,53 @@ __device__ bool pip_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   return (par & ~onb) != 0;
 }
 
-// class of a point from the class grid: 0 out, 1 in, 2 mixed (built for every map)
+// class of a point from the class grid: 0 out, 1 in, 2 mixed (built for every map); `cell`
+// and `word` are what pip_cell needs for a mixed cell
 template <typename T>
-__device__ __forceinline__ int fine_class(const Consts<T>& c, const Map<T>& m, T n, T e) {
+__device__ __forceinline__ int fine_lookup(const Consts<T>& c, const Map<T>& m, T n, T e, int& cell,
+                                           uint32_t& word) {
   const T fx = (e - c.fx0) * c.finvx, fy = (n - c.fy0) * c.finvy;
+  cell = 0;
+  word = 0;
   if (!(fx >= T(0) && fx < T(kFine) && fy >= T(0) && fy < T(kFine))) return 0;
-  const int cell = (int)fy * kFine + (int)fx;
-  return (m.fine[cell >> 4] >> ((cell & 15) * 2)) & 3;
+  cell = (int)fy * kFine + (int)fx;
+  word = m.fine[cell >> 4];
+  return (word >> ((cell & 15) * 2)) & 3;
 }
 
-// Polygon.contains(Point(e, n)): fine-grid class when the cell is pure, band scan otherwise
+template <typename T>
+__device__ __forceinline__ int fine_class(const Consts<T>& c, const Map<T>& m, T n, T e) {
+  int cell;
+  uint32_t word;
+  return fine_lookup(c, m, n, e, cell, word);
+}
+
+// Polygon.contains(Point(e, n)) for a point in mixed class cell `cell` (class word `word`):
+// the cell's constant crossing parity plus GEOS's count over the cell's live edges only
+template <typename T>
+__device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t word, T n, T e) {
+  const uint32_t mixed = (word >> 1) & 0x55555555u;
+  const int r = m.frank[cell >> 4] + __popc(mixed & ((1u << ((cell & 15) * 2)) - 1u));
+  const uint2 rec = m.crec[r];
+  uint32_t par = rec.x, onb = 0;
+  const int first = (int)(rec.y & 0xffffu), cnt = (int)(rec.y >> 16);
+#pragma unroll 1
+  for (int k = 0; k < cnt; ++k) {
+    const Edge<T> g = m.edge[m.clive[first + k]];
+    count_segment(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
+  }
+  return (par & ~onb) != 0;
+}
+
+// Polygon.contains(Point(e, n)): fine-grid class when the cell is pure; the mixed cell's
+// record (or, without records, a band scan) otherwise
 template <typename T>
 __device__ bool pip_point(const Consts<T>& c, const Map<T>& m, T n, T e) {
-  const int cls = fine_class(c, m, n, e);
+  int cell;
+  uint32_t word;
+  const int cls = fine_lookup(c, m, n, e, cell, word);
   if (cls < 2) return cls == 1;
+  if (m.use_cells) return pip_cell(m, cell, word, n, e);
   return pip_indexed(c, m, n, e);
 }
 
@@ -490,7 +533,21 @@ template <typename T>
 __device__ bool hull_in_terrain(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst) {
   if (dobst > c.hull_safe) return pip_point(c, m, n, e);
   const T h = c.half_len;
-  // near shore: each corner by its fine-grid class, band scans only for corners in mixed cells
+  // near shore: each corner by its fine-grid class; a corner in a mixed cell by the cell's
+  // record (or a band scan without records)
+  if (m.use_cells) {
+    int l00, l01, l10, l11;
+    uint32_t w00, w01, w10, w11;
+    const int c00 = fine_lookup(c, m, n - h, e - h, l00, w00), c01 = fine_lookup(c, m, n - h, e + h, l01, w01);
+    const int c10 = fine_lookup(c, m, n + h, e - h, l10, w10), c11 = fine_lookup(c, m, n + h, e + h, l11, w11);
+    if (c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1) return true;
+    bool hit = false;
+    if (c00 == 2) hit |= pip_cell(m, l00, w00, n - h, e - h);
+    if (c01 == 2) hit |= pip_cell(m, l01, w01, n - h, e + h);
+    if (c10 == 2) hit |= pip_cell(m, l10, w10, n + h, e - h);
+    if (c11 == 2) hit |= pip_cell(m, l11, w11, n + h, e + h);
+    return hit;
+  }
   const int c00 = fine_class(c, m, n - h, e - h), c01 = fine_class(c, m, n - h, e + h);
   const int c10 = fine_class(c, m, n + h, e - h), c11 = fine_class(c, m, n + h, e + h);
   if (c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1) return true;

@@ -139,6 +139,9 @@ __device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* ds
   m.edge = reinterpret_cast<const Edge<T>*>(dst);
   m.idx = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.idx) - src));
   m.fine = reinterpret_cast<const uint32_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.fine) - src));
+  m.frank = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.frank) - src));
+  m.crec = reinterpret_cast<const uint2*>(dst + (reinterpret_cast<const unsigned char*>(a.map.crec) - src));
+  m.clive = reinterpret_cast<const uint8_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.clive) - src));
   return m;
 }
 
@@ -227,6 +230,11 @@ struct Xchg {
 __device__ unsigned long long g_sit_diag[2][32];
 #endif
 #ifdef SIT_DIAG_PHASES
+// per wave of the last launch: start / end (realtime ticks), shader cycles, HW_ID | XCC_ID << 32
+constexpr int kDiagWaves = 8192;
+__device__ unsigned long long g_sit_wave[kDiagWaves][4];
+#endif
+#ifdef SIT_DIAG_PHASES
 // the fence makes the ship state live in registers at the timer, so arithmetic cannot be
 // sunk across a phase boundary
 template <typename T>
@@ -311,6 +319,10 @@ template <typename T, bool SYNTH, bool LDSMAP>
 __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Xchg<T> xs[2];
+#ifdef SIT_DIAG_PHASES
+  const unsigned long long w_t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long w_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // The ~70 per-step constants go kernel arguments -> LDS -> VGPRs: loaded through LDS they
   // land in vector registers (one wave per SIMD leaves ~512 per lane, AGPRs included), whereas
   // kernel-argument constants compete for the 102 SGPRs and spill to VGPR lanes (v_readlane
@@ -603,6 +615,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #ifdef SIT_DIAG_PHASES
   if (lane == 0)
     for (int k = 0; k < 7; ++k) atomicAdd(&g_sit_diag[type][16 + k], ph[k]);
+  const unsigned long long w_loop = ph_t;
 #endif
 
   // ---------------- write back ----------------
@@ -619,6 +632,30 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       a.st.episodes[env] = episodes;
     }
   }
+#ifdef SIT_DIAG_PHASES
+  // whole-wave timing: [24] sum of wave cycles, [25] max wave cycles, [26] sum of prologue
+  // cycles, [27] sum of epilogue cycles, [28]/[29] min/max start (realtime), [30]/[31] min/max end
+  if (lane == 0) {
+    const unsigned long long w_t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long w_r1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* g = g_sit_diag[type];
+    atomicAdd(&g[24], w_t1 - w_t0);
+    atomicMax(&g[25], w_t1 - w_t0);
+    atomicAdd(&g[26], w_loop - w_t0 - (ph[0] + ph[1] + ph[2] + ph[3] + ph[4] + ph[5] + ph[6]));
+    atomicAdd(&g[27], w_t1 - w_loop);
+    atomicMin(&g[28], w_r0);
+    atomicMax(&g[29], w_r0);
+    atomicMin(&g[30], w_r1);
+    atomicMax(&g[31], w_r1);
+    const int wid = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    if (wid < kDiagWaves) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);     // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);   // HW_REG_XCC_ID
+      g_sit_wave[wid][0] = w_r0; g_sit_wave[wid][1] = w_r1; g_sit_wave[wid][2] = w_t1 - w_t0;
+      g_sit_wave[wid][3] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    }
+  }
+#endif
 }
 
 // MultiShipRLEnv.init_step for masked envs (one thread per ship)
@@ -671,6 +708,20 @@ __global__ __launch_bounds__(256) void k_reset(const KArgs<T> a, const uint8_t* 
       initial_state[(size_t)env * SIT_OBS_DIM + j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
 }
 
+// map predicates of arbitrary points (test/diagnostic entry sit_probe_map, one thread per
+// point): boundary distance, Polygon.contains of the point, is_pos_inside_obstacles hull test
+template <typename T>
+__global__ __launch_bounds__(256) void k_probe_map(const KArgs<T> a, int n, const T* pts, T* dist,
+                                                   uint8_t* inside, uint8_t* hull) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const T pn = pts[2 * i], pe = pts[2 * i + 1];
+  const T d = distance_indexed(a.c, a.map, pn, pe);
+  if (dist) dist[i] = d;
+  if (inside) inside[i] = pip_point(a.c, a.map, pn, pe) ? 1 : 0;
+  if (hull) hull[i] = hull_in_terrain(a.c, a.map, pn, pe, d) ? 1 : 0;
+}
+
 // construction-time state (one thread per env)
 template <typename T>
 __global__ __launch_bounds__(256) void k_restart(const KArgs<T> a) {
@@ -719,7 +770,9 @@ struct sit_handle {
   // map
   unsigned char* map = nullptr;
   int n_poly = 0, n_vert = 0;
-  size_t map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0;
+  size_t map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0, map_frank = 0, map_crec = 0, map_clive = 0;
+  int use_cells = 0;
+  int64_t n_mixed = 0, n_live = 0;
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
@@ -873,6 +926,10 @@ KArgs<T> make_args(const sit_handle* h) {
   a.map.edge = reinterpret_cast<const Edge<T>*>(h->map);
   a.map.idx = reinterpret_cast<const uint16_t*>(h->map + h->map_idx);
   a.map.fine = reinterpret_cast<const uint32_t*>(h->map + h->map_fine);
+  a.map.frank = reinterpret_cast<const uint16_t*>(h->map + h->map_frank);
+  a.map.crec = reinterpret_cast<const uint2*>(h->map + h->map_crec);
+  a.map.clive = reinterpret_cast<const uint8_t*>(h->map + h->map_clive);
+  a.map.use_cells = h->use_cells;
   a.map.off = reinterpret_cast<const int32_t*>(h->map + h->map_off);
   a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
   a.map_bytes = (int32_t)h->map_bytes;
@@ -926,16 +983,54 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
 extern "C" {
 
 #if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
+#ifdef SIT_DIAG_PHASES
+int sit_diag_read_waves(unsigned long long* out, int n) {   // [n][4], diagnostic builds only
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (n > kDiagWaves) n = kDiagWaves;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sit_wave), sizeof(unsigned long long) * 4 * n) != hipSuccess) return -1;
+  return 0;
+}
+#endif
 int sit_diag_read(unsigned long long* out, int reset) {   // diagnostic builds only
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sit_diag), sizeof(g_sit_diag)) != hipSuccess) return -1;
   if (reset) {
     unsigned long long z[2][32] = {};
+    for (int t = 0; t < 2; ++t) z[t][28] = z[t][30] = ~0ull;
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_sit_diag), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;
 }
 #endif
+
+int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint8_t* inside, uint8_t* hull,
+                  void* stream) {
+  if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
+  if (!h->have_map) return fail(h, SIT_E_STATE, "sit_load_map has not been called");
+  if (n < 0 || (n > 0 && !pts_ne)) return fail(h, SIT_E_INVALID, "need n >= 0 points");
+  if (n == 0) return SIT_OK;
+  const int blocks = (n + 255) / 256;
+  if (h->precision == SIT_F64) {
+    const KArgs<double> a = make_args<double>(h);
+    hipLaunchKernelGGL(k_probe_map<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, n,
+                       (const double*)pts_ne, (double*)dist, inside, hull);
+  } else {
+    const KArgs<float> a = make_args<float>(h);
+    hipLaunchKernelGGL(k_probe_map<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, n,
+                       (const float*)pts_ne, (float*)dist, inside, hull);
+  }
+  HIP_TRY(h, hipGetLastError());
+  return SIT_OK;
+}
+
+int sit_map_info(const sit_handle* h, int64_t* info, int32_t n) {
+  if (!h || !info || n < 0) return SIT_E_INVALID;
+  if (!h->have_map) return SIT_E_STATE;
+  const int64_t v[6] = {(int64_t)h->map_bytes, h->n_mixed, h->n_live, h->use_index, h->use_cells,
+                        (int64_t)map_lds_bytes(h)};
+  for (int i = 0; i < n && i < 6; ++i) info[i] = v[i];
+  return SIT_OK;
+}
 
 int32_t sit_abi_version(void) { return SIT_ABI_VERSION; }
 size_t sit_params_size(void) { return sizeof(sit_params); }
@@ -1170,6 +1265,54 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
       fine[cell >> 4] |= k << ((cell & 15) * 2);
     }
   h->fx0 = fx0; h->fy0 = fy0; h->finvx = 1.0 / fsx; h->finvy = 1.0 / fsy;
+  // point-in-polygon records of the mixed cells (see Map in sit_device.h).  An edge's GEOS
+  // crossing contribution is the same for every point of cell [x0,x1]x[y0,y1] when (1 m
+  // margin, far above float rounding of coordinates <= 1e5 m): it lies wholly left of the cell
+  // (early return), its y-range misses the cell's rows, or it spans the rows strictly and,
+  // within them, lies wholly right or wholly left of the cell (then it straddles every row and
+  // its orientation against every point is that against the centre).  All other edges are live.
+  std::vector<uint16_t> frank(kFineWords, 0);
+  std::vector<uint32_t> crec;
+  std::vector<uint8_t> clive;
+  {
+    int rank = 0;
+    for (int w = 0; w < kFineWords; ++w) {
+      frank[w] = (uint16_t)std::min(rank, 65535);
+      rank += __builtin_popcount((fine[w] >> 1) & 0x55555555u);
+    }
+    for (int cell = 0; cell < kFine * kFine; ++cell) {
+      if (((fine[cell >> 4] >> ((cell & 15) * 2)) & 3) != 2) continue;
+      const int i = cell % kFine, j = cell / kFine;
+      const double x0 = fx0 + i * fsx, x1 = fx0 + (i + 1) * fsx, y0 = fy0 + j * fsy, y1 = fy0 + (j + 1) * fsy;
+      const double cx = 0.5 * (x0 + x1), cy = 0.5 * (y0 + y1), mgn = 1.0;
+      uint32_t par = 0;
+      const size_t first = clive.size();
+      for (int e = 0; e < nv; ++e) {
+        const double p1x = vx[e], p1y = vy[e], p2x = bxv[e], p2y = byv[e];
+        const double xmax = std::max(p1x, p2x), ymin = std::min(p1y, p2y), ymax = std::max(p1y, p2y);
+        if (xmax < x0 - mgn) continue;                          // left of every point: no count
+        if (ymax < y0 - mgn || ymin > y1 + mgn) continue;       // never straddles a cell row
+        if (ymin < y0 - mgn && ymax > y1 + mgn) {
+          const double ta = (y0 - mgn - p1y) / (p2y - p1y), tb = (y1 + mgn - p1y) / (p2y - p1y);
+          const double xa = p1x + ta * (p2x - p1x), xb = p1x + tb * (p2x - p1x);
+          const bool right = std::min(xa, xb) > x1 + mgn && xmax > x1 + mgn;
+          const bool left = std::max(xa, xb) < x0 - mgn && xmax > x1 + mgn;
+          if (right || left) {
+            const double det = (p1x - cx) * (p2y - cy) - (p1y - cy) * (p2x - cx);
+            const int o = (det > 0) - (det < 0);
+            const int oo = (p2y < p1y) ? -o : o;
+            if (oo > 0) par ^= 1u << poly_of[e];
+            continue;
+          }
+        }
+        clive.push_back((uint8_t)e);
+      }
+      const size_t cnt = clive.size() - first;
+      crec.push_back(par);
+      crec.push_back((uint32_t)first | ((uint32_t)cnt << 16));
+    }
+  }
+  const bool cells_ok = crec.size() / 2 <= 65535 && clive.size() <= 65535;
   const size_t head = (size_t)kIdxHead;
   const size_t gbase = (head + bentries.size() + 3) & ~size_t(3);   // 8-byte aligned groups
   const size_t n_idx = gbase + gentries.size();
@@ -1191,6 +1334,12 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
   size_t o = align256(nv * esz);
   h->map_idx = o; o = align256(o + idx.size() * 2);
   h->map_fine = o; o = align256(o + fine.size() * 4);
+  h->use_cells = cells_ok ? 1 : 0;
+  h->n_mixed = (int64_t)crec.size() / 2;
+  h->n_live = (int64_t)clive.size();
+  h->map_frank = o; o += (cells_ok ? frank.size() * 2 : 0); o = (o + 7) & ~size_t(7);
+  h->map_crec = o; o += (cells_ok ? crec.size() * 4 : 0);
+  h->map_clive = o; o = align256(o + (cells_ok ? clive.size() : 0));
   h->map_bytes = o;
   h->map_off = o; o = align256(o + (n_poly + 1) * 4);
   h->map_bbox = o; o = align256(o + 4 * n_poly * rs);
@@ -1206,6 +1355,11 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
   }
   std::memcpy(host.data() + h->map_idx, idx.data(), idx.size() * 2);
   std::memcpy(host.data() + h->map_fine, fine.data(), fine.size() * 4);
+  if (cells_ok) {
+    std::memcpy(host.data() + h->map_frank, frank.data(), frank.size() * 2);
+    std::memcpy(host.data() + h->map_crec, crec.data(), crec.size() * 4);
+    if (!clive.empty()) std::memcpy(host.data() + h->map_clive, clive.data(), clive.size());
+  }
   std::memcpy(host.data() + h->map_off, offs.data(), (n_poly + 1) * 4);
   for (size_t i = 0; i < bbox.size(); ++i) {
     if (rs == 8) reinterpret_cast<double*>(host.data() + h->map_bbox)[i] = bbox[i];

@@ -113,6 +113,26 @@ class VecMultiShipRLEnv:
             return None
         return self._dev(mask, torch.uint8, (self.n_env,), "mask")
 
+    # ---------------- map diagnostics ----------------
+    def map_info(self) -> dict:
+        """Spatial-index statistics of the loaded island map (sit_map_info)."""
+        info = (c_int64 * 6)()
+        self._call("sit_map_info", info, 6)
+        keys = ("map_bytes", "mixed_cells", "live_edges", "use_index", "use_cells", "lds_bytes")
+        return dict(zip(keys, (int(v) for v in info)))
+
+    def probe_map(self, pts_ne):
+        """The step kernel's map predicates at arbitrary (north, east) points: boundary distance,
+        Polygon.contains and the 4-corner hull test (sit_probe_map)."""
+        pts = self._dev(pts_ne, self.dtype, (-1, 2), "pts_ne")
+        n = pts.shape[0]
+        dist = torch.empty(n, dtype=self.dtype, device=self.device)
+        inside = torch.empty(n, dtype=torch.uint8, device=self.device)
+        hull = torch.empty(n, dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            self._call("sit_probe_map", n, _ptr(pts), _ptr(dist), _ptr(inside), _ptr(hull), self._stream())
+        return dist, inside.bool(), hull.bool()
+
     # ---------------- env API ----------------
     def restart(self):
         """Construction-time state (as if freshly built)."""
