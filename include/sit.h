@@ -78,6 +78,7 @@ extern "C" {
 #define SIT_ST_COLLISION (1u << 11)      /* "|Ship collision|"                         */
 #define SIT_ST_TEST_DONE (1u << 12)      /* test ship terminal  (else "|Test ship not in terminal state|")     */
 #define SIT_ST_OBS_DONE (1u << 13)       /* obstacle ship terminal (else "|Obstacle ship not in terminal state|") */
+#define SIT_ST_NO_STEP (1u << 30)        /* policy mode: the env waited for its action; no step taken in this row */
 #define SIT_ST_ROUTE_OVERFLOW (1u << 31) /* IW insertion dropped: route table full (no reference counterpart) */
 
 /* ---- next_state layout (MSRL_Env.py:426-437) --------------------------------------- */
@@ -279,8 +280,27 @@ typedef struct sit_rollout_args {
   int32_t* transition_count;  /* int32[1] */
   int32_t transition_capacity;
   int32_t mask_horizon;       /* args.num_steps_episode (main_ast.py:71, 387); 0 = none */
+  /* Policy mode (action_ne == NULL, policy_action != NULL): the actions of sampling events come
+   * from a policy evaluated between launches (the SAC actor, agent.select_action mode 1,
+   * main_ast.py:344-349).  At a sampling event an env consumes policy_action[e] if
+   * policy_ready[e] != 0 (route angle a = policy_action[e] * pi/6, IW as in the synthetic
+   * sampler; policy_ready[e] is cleared); otherwise it takes no further step in this launch
+   * (its rows get status SIT_ST_NO_STEP and done 0) and queues a request: request_env[q] = e,
+   * request_noise[q] = N(0,1) from Philox4x32-10(key = seed, counter = (env_id, event, 0x504F, 0))
+   * (Box-Muller), q = atomicAdd(request_count) (requests beyond request_capacity are dropped
+   * and re-issued by the next launch).  The caller runs the policy on the queued envs'
+   * observations (state field last_obs) and writes policy_action / policy_ready before the
+   * next launch.  Per-env trajectories equal those of a synchronous per-step loop. */
+  const void* policy_action;  /* real[n_env] in [-1, 1] */
+  int32_t* policy_ready;      /* int32[n_env] */
+  int32_t* request_env;       /* int32[request_capacity] */
+  void* request_noise;        /* real[request_capacity] */
+  int32_t* request_count;     /* int32[1] */
+  int32_t request_capacity;
+  int64_t* env_steps;         /* int64[1] or NULL: += env-steps executed (policy mode) */
 } sit_rollout_args;
 int sit_rollout(sit_handle* h, const sit_rollout_args* a, void* stream);
+size_t sit_rollout_args_size(void);
 
 /* ---- state export / import (device blob) ------------------------------------------ */
 /* The dynamic state of all envs (ship states, controller integrators, route tables,

@@ -26,6 +26,7 @@ ST_TEST_MECHANICAL, ST_TEST_NAVIGATION, ST_TEST_BLACKOUT = 1 << 3, 1 << 4, 1 << 
 ST_OBS_ENDPOINT, ST_OBS_HORIZON, ST_OBS_TERRAIN = 1 << 6, 1 << 7, 1 << 8
 ST_OBS_IW_TERMINAL, ST_OBS_NAVIGATION, ST_COLLISION = 1 << 9, 1 << 10, 1 << 11
 ST_TEST_DONE, ST_OBS_DONE, ST_ROUTE_OVERFLOW = 1 << 12, 1 << 13, 1 << 31
+ST_NO_STEP = 1 << 30
 
 _D = c_double
 PARAM_FIELDS = [
@@ -73,6 +74,9 @@ class RolloutArgs(ctypes.Structure):
         ("action_out", c_void_p), ("done_count", c_void_p),
         ("transitions", c_void_p), ("transition_count", c_void_p), ("transition_capacity", c_int32),
         ("mask_horizon", c_int32),
+        ("policy_action", c_void_p), ("policy_ready", c_void_p), ("request_env", c_void_p),
+        ("request_noise", c_void_p), ("request_count", c_void_p), ("request_capacity", c_int32),
+        ("env_steps", c_void_p),
     ]
 
 
@@ -84,6 +88,7 @@ class SitError(RuntimeError):
 SIGNATURES = {
     "sit_abi_version": (c_int32, []),
     "sit_params_size": (c_size_t, []),
+    "sit_rollout_args_size": (c_size_t, []),
     "sit_params_default": (None, [POINTER(SitParams)]),
     "sit_create": (c_int32, [POINTER(SitParams), c_int32, c_int32, c_int32, POINTER(c_void_p)]),
     "sit_destroy": (None, [c_void_p]),
@@ -130,6 +135,9 @@ def load():
     if lib.sit_params_size() != ctypes.sizeof(SitParams):
         raise ImportError(f"sit_params layout mismatch: C {lib.sit_params_size()} vs "
                           f"ctypes {ctypes.sizeof(SitParams)} bytes")
+    if lib.sit_rollout_args_size() != ctypes.sizeof(RolloutArgs):
+        raise ImportError(f"sit_rollout_args layout mismatch: C {lib.sit_rollout_args_size()} vs "
+                          f"ctypes {ctypes.sizeof(RolloutArgs)} bytes")
     _lib = lib
     return lib
 

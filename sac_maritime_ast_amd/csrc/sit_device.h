@@ -164,6 +164,16 @@ __device__ __forceinline__ double sampler_uniform(uint64_t seed, uint64_t env_id
   return (hi * 67108864.0 + lo) * (1.0 / 9007199254740992.0);
 }
 
+// standard normal from Philox(key=seed, ctr=(env_id, event, 0x504F, 0)) by Box-Muller (two
+// 53-bit uniforms, u1 in (0, 1]): the policy's reparameterisation noise of a sampling event
+__device__ __forceinline__ double sampler_normal(uint64_t seed, uint64_t env_id, uint32_t event) {
+  uint32_t c[4] = {(uint32_t)env_id, event, 0x504Fu, 0u};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const double u1 = ((double)(c[0] >> 5) * 67108864.0 + (double)(c[1] >> 6) + 1.0) * (1.0 / 9007199254740992.0);
+  const double u2 = ((double)(c[2] >> 5) * 67108864.0 + (double)(c[3] >> 6)) * (1.0 / 9007199254740992.0);
+  return sqrt(-2.0 * log(u1)) * cos(2.0 * M_PI * u2);
+}
+
 // --------------------------------------------------------------------------------------
 // route access: the body of a ship's route (waypoints 0 .. n_wpt-2) lives in a column of a
 // [cap][stride] table (global or LDS); the final waypoint is held in registers because
@@ -181,9 +191,23 @@ struct Route {
   int nw;         // current number of waypoints
   T pn, pe;       // waypoint k-1
   T cn, ce;       // waypoint k
+  // the leg's path-tangential angle and its sine/cosine (LOS_guidance.py:110-113) depend only
+  // on the two waypoints: computed when the leg changes, not every step (same values)
+  T alpha, sa, ca;
   __device__ __forceinline__ T n(int i) const { return (i >= nw - 1) ? end_n : tn[i * stride]; }
   __device__ __forceinline__ T e(int i) const { return (i >= nw - 1) ? end_e : te[i * stride]; }
-  __device__ __forceinline__ void load_leg(int k) { pn = n(k - 1); pe = e(k - 1); cn = n(k); ce = e(k); }
+  __device__ __forceinline__ void leg_geometry() {
+    const T dx = cn - pn, dy = ce - pe;
+    alpha = xatan2(dy, dx);
+    const T len = xsqrt(dx * dx + dy * dy);
+    sa = T(0);
+    ca = T(1);
+    if (len > T(0)) { sa = dy / len; ca = dx / len; }
+  }
+  __device__ __forceinline__ void load_leg(int k) {
+    pn = n(k - 1); pe = e(k - 1); cn = n(k); ce = e(k);
+    leg_geometry();
+  }
   // update_route: insert (in_, ie) at index -1 (controllers.py:298-303); false on overflow
   __device__ __forceinline__ bool insert(T in_, T ie, int k, int cap) {
     if (nw >= cap) return false;
@@ -191,7 +215,7 @@ struct Route {
     tn[i * stride] = in_;
     te[i * stride] = ie;
     nw += 1;
-    if (k == i) { cn = in_; ce = ie; }   // the leg pointed at the final waypoint
+    if (k == i) { cn = in_; ce = ie; leg_geometry(); }   // the leg pointed at the final waypoint
     return true;
   }
 };
@@ -226,14 +250,11 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
       s.k += 1;
       rt.pn = rt.cn; rt.pe = rt.ce;
       rt.cn = rt.n(s.k); rt.ce = rt.e(s.k);
+      rt.leg_geometry();
     }
   }
   const T pn = rt.pn, pe = rt.pe;
-  const T dx = rt.cn - pn, dy = rt.ce - pe;
-  const T alpha = xatan2(dy, dx);
-  const T len = xsqrt(dx * dx + dy * dy);
-  T sa = T(0), ca = T(1);
-  if (len > T(0)) { sa = dy / len; ca = dx / len; }
+  const T alpha = rt.alpha, sa = rt.sa, ca = rt.ca;
   T ect = -(s.n - pn) * sa + (s.e - pe) * ca;
   ect_abs = xabs(ect);
   if (ect * ect >= c.los_r2) ect = c.los_clamp;           // sign lost (Q5)

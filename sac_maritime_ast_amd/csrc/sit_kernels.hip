@@ -113,6 +113,14 @@ struct StepIO {
   int32_t* transition_count;
   int32_t transition_capacity;
   int32_t mask_horizon;
+  // policy mode (kPolicy): per-env action slots and the request queue of waiting envs
+  const T* policy_action;
+  int32_t* policy_ready;
+  int32_t* request_env;
+  T* request_noise;
+  int32_t* request_count;
+  int32_t request_capacity;
+  unsigned long long* env_steps;
 };
 
 template <typename T>
@@ -222,7 +230,10 @@ struct Xchg {
 
 // ---------------------------------------------------------------------------------------
 // the env step kernel: K steps of MultiShipRLEnv.step (+ optional auto-reset)
-//   SYNTH : actions from the synthetic AST sampler (else explicit arrays)
+//   MODE  : kExplicit = caller's action arrays, kSynth = synthetic AST sampler on device,
+//           kPolicy = actions from a policy run between launches (an env that reaches a
+//           sampling event without a fresh action waits for the rest of the launch and queues
+//           a request; the next launch consumes the action the policy wrote for it)
 // ---------------------------------------------------------------------------------------
 #if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
 // Diagnostic builds only (tools/diag_paths.py): [type][0..15] predicate path statistics,
@@ -315,7 +326,10 @@ __device__ void diag_wave(int type, int lane, bool act, const int* v) {
 __device__ __forceinline__ void store2(float* p, float a, float b) { *reinterpret_cast<float2*>(p) = make_float2(a, b); }
 __device__ __forceinline__ void store2(double* p, double a, double b) { *reinterpret_cast<double2*>(p) = make_double2(a, b); }
 
-template <typename T, bool SYNTH, bool LDSMAP>
+constexpr int kExplicit = 0, kSynth = 1, kPolicy = 2;
+constexpr uint32_t kSampGeBit = 1u << 28;   // exchange-only: obstacle sampling distance >= AB_len
+
+template <typename T, int MODE, bool LDSMAP>
 __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Xchg<T> xs[2];
@@ -357,6 +371,16 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   double ab_len = 0.0, ab_alpha = 0.0;
   T lo[6] = {};                      // this ship's part of the last observation
   const int lo_base = type == 0 ? 0 : 6, lo_n = type == 0 ? 6 : 4;
+  // policy mode: both lanes of an env track whether its next step is a sampling event
+  bool need = false, ready = false, stalled = false;
+  T pa = T(0);
+  uint32_t n_stepped = 0;
+  if (MODE == kPolicy && act) {
+    const double samp0 = (double)a.st.env[0][env];
+    need = a.st.ep_step[env] == 0 || (samp0 >= a.sc.ab_len[env] && a.st.stop[n_env + env] == 0);
+    ready = a.io.policy_ready[env] != 0;
+    pa = a.io.policy_action[env];
+  }
   if (act) {
     for (int j = 0; j < lo_n; ++j) lo[j] = a.st.last_obs[(size_t)(lo_base + j) * n_env + env];
     ep_step = a.st.ep_step[env];
@@ -398,10 +422,33 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #endif
     bool sac = false, init_f = false;
     double ang = NAN;
-    if (act) {
+    if (MODE == kPolicy && act && !stalled && need && !ready) {
+      // sampling event without an action: wait for the policy; the obstacle lane queues the
+      // request with this event's standard-normal draw (reparameterised sample, normal.py:96-101)
+      stalled = true;
+      if (type == 1) {
+        const int q = atomicAdd(a.io.request_count, 1);
+        if (q < a.io.request_capacity) {
+          a.io.request_env[q] = env;
+          a.io.request_noise[q] = (T)sampler_normal(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
+        }
+      }
+    }
+    const bool live = act && !stalled;
+    if (live) {
+      ++n_stepped;
       if (type == 1) {
         // converted_action / SAC_update / init of this step
-        if (SYNTH) {
+        if (MODE == kPolicy) {
+          init_f = (ep_step == 0);
+          sac = need;
+          if (sac) {                     // the policy's squashed action scales the route angle
+            ang = (double)pa * (M_PI / 6.0);
+            iwn = (T)((double)s.n + ab_len * cos(ab_alpha + ang));
+            iwe = (T)((double)s.e + ab_len * sin(ab_alpha + ang));
+            ++event;
+          }
+        } else if (MODE == kSynth) {
           init_f = (ep_step == 0);
           sac = init_f || ((double)samp >= ab_len && !s.stop);
           if (sac) {
@@ -532,7 +579,8 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       }
       x.n[type][lane] = s.n;
       x.e[type][lane] = s.e;
-      x.bits[type][lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u);
+      x.bits[type][lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u) |
+                           ((type == 1 && (double)samp >= ab_len) ? kSampGeBit : 0u);
       if (type == 1) { x.r_nto[lane] = r_nt; x.r_o[lane] = r_term; }
     }
     SIT_PH(3);
@@ -543,7 +591,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #endif
     // ---------------- env level: shared reward, outputs ----------------
     bool env_done = false;
-    if (act) {
+    if (MODE == kPolicy && act && !live && type == 0) {   // no step taken this row
+      if (a.io.status) a.io.status[row] = SIT_ST_NO_STEP;
+      if (a.io.done) a.io.done[row] = 0;
+    }
+    if (live) {
       const T dn = x.n[0][lane] - x.n[1][lane], de = x.e[0][lane] - x.e[1][lane];
       const bool coll = dn * dn + de * de < c.min_dist2;
       const uint32_t bt = x.bits[0][lane], bo = x.bits[1][lane];
@@ -554,8 +606,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         const T rs = coll ? T(2000) : T(0);
         const T reward = r_nt + r_term + x.r_nto[lane] + x.r_o[lane] + r_snt + rs;
         const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
+#ifndef SIT_ABLATE_STORES
         if (a.io.reward) a.io.reward[row] = reward;
         if (a.io.done) a.io.done[row] = env_done ? 1 : 0;
+#endif
         const int slot = x.slot[lane];
         if (slot >= 0 && slot < a.io.transition_capacity) {
           T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
@@ -565,32 +619,48 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           const bool horizon_hit = a.io.mask_horizon > 0 && ep_step + 2 == a.io.mask_horizon;
           rec[22] = (horizon_hit || !env_done) ? T(1) : T(0);
         }
+#ifndef SIT_ABLATE_STORES
         if (a.io.status) a.io.status[row] = status;
+#endif
+#ifndef SIT_ABLATE_STORES
         if (a.io.next_state) {
           T* ns = a.io.next_state + row * SIT_OBS_DIM;
           store2(ns, s.n, s.e); store2(ns + 2, s.psi, o_rpm); store2(ns + 4, o_ect, o_pme);
         }
+#endif
       } else {
+#ifndef SIT_ABLATE_STORES
         if (a.io.next_state) {
           T* ns = a.io.next_state + row * SIT_OBS_DIM;
           store2(ns + 6, s.n, s.e); store2(ns + 8, s.psi, o_ect);
         }
+#endif
+#ifndef SIT_ABLATE_STORES
         if (a.io.action_out) {
           T* ao = a.io.action_out + row * 4;
           store2(ao, iwn, iwe); store2(ao + 2, (T)ang, sac ? T(1) : T(0));
         }
+#endif
         const int slot = x.slot[lane];
         if (slot >= 0 && slot < a.io.transition_capacity) {
           T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
           for (int j = 0; j < 4; ++j) rec[6 + j] = lo[j];
           rec[10] = (T)ang;
           rec[18] = s.n; rec[19] = s.e; rec[20] = s.psi; rec[21] = o_ect;
+          if (MODE == kPolicy) rec[10] = pa;   // the policy's action (memory.push, main_ast.py:395)
           rec[23] = (T)(a.io.env_id_offset + env);
         }
       }
       // the observation becomes the next step's state
       if (type == 0) { lo[0] = s.n; lo[1] = s.e; lo[2] = s.psi; lo[3] = o_rpm; lo[4] = o_ect; lo[5] = o_pme; }
       else { lo[0] = s.n; lo[1] = s.e; lo[2] = s.psi; lo[3] = o_ect; }
+      if (MODE == kPolicy) {
+        if (sac) ready = false;        // the action was consumed
+        // the next step is a sampling event at an episode start or once the sampling distance
+        // reaches AB_len while the obstacle ship runs (the obstacle lane's own test, exchanged)
+        const bool obs_stop = (bo & kStopBit) || coll;
+        need = ((bo & kSampGeBit) && !obs_stop) || (a.io.auto_reset && env_done);
+      }
     }
     // episode-done count: one ballot + popcount per wave, one atomic per wave
     if (type == 0 && a.io.done_count) {
@@ -599,9 +669,13 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     }
     SIT_PH(5);
     // ---------------- auto reset: reset() + init_step() (test_beds/main_ast.py:314-329) ----------------
-    if (act) {
+    if (live) {
       ep_step += 1;
+#ifdef SIT_ABLATE_RESET
+      if (false) {
+#else
       if (a.io.auto_reset && env_done) {
+#endif
         reset_ship(a.sc, type, env, n_env, s, rt.nw);
         rt.load_leg(s.k);
         ep_step = 0;
@@ -619,6 +693,14 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #endif
 
   // ---------------- write back ----------------
+  if (MODE == kPolicy) {
+    if (act && type == 1) a.io.policy_ready[env] = ready ? 1 : 0;
+    if (a.io.env_steps && type == 0) {   // env-steps executed: one atomic per wave
+      unsigned long long v = act ? n_stepped : 0;
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0 && v) atomicAdd(a.io.env_steps, v);
+    }
+  }
   if (act) {
     store_ship(a.st, sid, s);
     a.st.nw[sid] = rt.nw;
@@ -944,8 +1026,9 @@ int ready(sit_handle* h) {
   return SIT_OK;
 }
 
-// LDS budget of one step-kernel block: above 64 KB a block measured ~1.75x slower
-constexpr size_t kLdsBudget = 64 * 1024;
+// LDS budget of one step-kernel block: two blocks (4 waves, one per SIMD) must fit the CU's
+// 160 KB; above 80 KB only one block fits and the grid runs in two rounds (~1.75x slower)
+constexpr size_t kLdsBudget = 80 * 1024;
 size_t map_lds_bytes(const sit_handle* h) { return (h->map_bytes + 255) & ~size_t(255); }
 
 template <typename T>
@@ -953,24 +1036,22 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   KArgs<T> a = make_args<T>(h);
   a.io = io;
   const int blocks = (h->n_env + kEnvsPerBlock - 1) / kEnvsPerBlock;
-  const bool synth = io.action_ne == nullptr;
+  const int mode = io.action_ne ? kExplicit : (io.policy_action ? kPolicy : kSynth);
   // the map (edges, index, classes) is staged in LDS when it fits the budget next to the
   // static exchange buffers; otherwise the predicates read it through the caches
   const size_t stat = sizeof(Xchg<T>) * 2 + sizeof(Consts<T>) + 256;
   const bool lds_map = map_lds_bytes(h) + stat <= kLdsBudget;
   const size_t lds = lds_map ? map_lds_bytes(h) : 0;
-  if (lds_map) {
-    const void* fn = synth ? (const void*)k_env_steps<T, true, true> : (const void*)k_env_steps<T, false, true>;
-    HIP_TRY(h, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  }
-  if (synth && lds_map)
-    hipLaunchKernelGGL((k_env_steps<T, true, true>), dim3(blocks), dim3(128), lds, stream, a);
-  else if (synth)
-    hipLaunchKernelGGL((k_env_steps<T, true, false>), dim3(blocks), dim3(128), 0, stream, a);
-  else if (lds_map)
-    hipLaunchKernelGGL((k_env_steps<T, false, true>), dim3(blocks), dim3(128), lds, stream, a);
-  else
-    hipLaunchKernelGGL((k_env_steps<T, false, false>), dim3(blocks), dim3(128), 0, stream, a);
+  auto go = [&](auto kern) -> int {
+    if (lds_map) HIP_TRY(h, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(128), lds, stream, a);
+    return SIT_OK;
+  };
+  int rc;
+  if (mode == kSynth) rc = lds_map ? go(k_env_steps<T, kSynth, true>) : go(k_env_steps<T, kSynth, false>);
+  else if (mode == kPolicy) rc = lds_map ? go(k_env_steps<T, kPolicy, true>) : go(k_env_steps<T, kPolicy, false>);
+  else rc = lds_map ? go(k_env_steps<T, kExplicit, true>) : go(k_env_steps<T, kExplicit, false>);
+  if (rc) return rc;
   HIP_TRY(h, hipGetLastError());
   return SIT_OK;
 }
@@ -1033,6 +1114,7 @@ int sit_map_info(const sit_handle* h, int64_t* info, int32_t n) {
 }
 
 int32_t sit_abi_version(void) { return SIT_ABI_VERSION; }
+size_t sit_rollout_args_size(void) { return sizeof(sit_rollout_args); }
 size_t sit_params_size(void) { return sizeof(sit_params); }
 
 void sit_params_default(sit_params* p) {
@@ -1214,6 +1296,8 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
   std::vector<uint16_t> gentries, bentries;
   std::vector<uint32_t> gstart(kGrid * kGrid + 1), bstart(kBands + 1);
   std::vector<double> dcell(nv);
+  std::vector<int> cand;
+  constexpr int kSamples = 64;   // per cell side for the candidate refinement
   for (int j = 0; j < kGrid; ++j)
     for (int i = 0; i < kGrid; ++i) {
       const double cx = gx0 + (i + 0.5) * sx, cy = gy0 + (j + 0.5) * sy;
@@ -1221,8 +1305,34 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
       for (int e = 0; e < nv; ++e) { dcell[e] = seg_dist(cx, cy, e); D = std::min(D, dcell[e] + hd); }
       gstart[j * kGrid + i] = (uint32_t)gentries.size();
       const size_t first = gentries.size();
+      // conservative prefilter, then the Lipschitz refinement: for every point p of the cell
+      // grown by 1 m, some sample s lies within r; the nearest edge e* of p has
+      // d_e*(s) <= d*(p) + r and min_f d_f(s) >= d*(p) - r, so e* is kept by
+      // d_e(s) <= min_f d_f(s) + 2r + 1 m at some sample.  A dropped edge is >= 1 m farther than
+      // the nearest at every point of the grown cell, so float rounding cannot make it the
+      // minimum: the minimum over the list equals the full scan's.
+      cand.clear();
       for (int e = 0; e < nv; ++e)
-        if (dcell[e] - hd <= D + 1.0) gentries.push_back((uint16_t)e);
+        if (dcell[e] - hd <= D + 1.0) cand.push_back(e);
+      if (cand.size() > 1) {
+        const double x0 = gx0 + i * sx - 1.0, y0 = gy0 + j * sy - 1.0;
+        const double dx = (sx + 2.0) / kSamples, dy = (sy + 2.0) / kSamples;
+        const double r2 = std::sqrt(dx * dx + dy * dy) + 1.0;   // 2r + 1 m
+        std::vector<char> keep(cand.size(), 0);
+        std::vector<double> dd(cand.size());
+        for (int v = 0; v < kSamples; ++v)
+          for (int u = 0; u < kSamples; ++u) {
+            const double px = x0 + (u + 0.5) * dx, py = y0 + (v + 0.5) * dy;
+            double m = INFINITY;
+            for (size_t q = 0; q < cand.size(); ++q) { dd[q] = seg_dist(px, py, cand[q]); m = std::min(m, dd[q]); }
+            for (size_t q = 0; q < cand.size(); ++q) keep[q] |= dd[q] <= m + r2;
+          }
+        size_t w = 0;
+        for (size_t q = 0; q < cand.size(); ++q)
+          if (keep[q]) cand[w++] = cand[q];
+        cand.resize(w);
+      }
+      for (int e : cand) gentries.push_back((uint16_t)e);
       while ((gentries.size() - first) % 4) gentries.push_back(gentries[first]);
     }
   gstart[kGrid * kGrid] = (uint32_t)gentries.size();
@@ -1534,6 +1644,12 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     return fail(h, SIT_E_INVALID, "next_state and action_out must be aligned to 2 reals");
   if (ra->transitions && (!ra->transition_count || ra->transition_capacity <= 0))
     return fail(h, SIT_E_INVALID, "transitions need transition_count and a positive capacity");
+  if (ra->policy_action && ra->action_ne)
+    return fail(h, SIT_E_INVALID, "policy mode and explicit actions are exclusive");
+  if (ra->policy_action && (!ra->policy_ready || !ra->request_env || !ra->request_noise ||
+                            !ra->request_count || ra->request_capacity <= 0))
+    return fail(h, SIT_E_INVALID, "policy mode needs policy_ready, request_env, request_noise, "
+                                  "request_count and a positive request_capacity");
   auto fill = [&](auto* io, auto* tag) {
     using R = std::remove_pointer_t<decltype(tag)>;
     io->n_steps = ra->n_steps; io->auto_reset = ra->auto_reset; io->seed = ra->seed;
@@ -1543,6 +1659,10 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     io->status = ra->status; io->action_out = (R*)ra->action_out; io->done_count = ra->done_count;
     io->transitions = (R*)ra->transitions; io->transition_count = ra->transition_count;
     io->transition_capacity = ra->transition_capacity; io->mask_horizon = ra->mask_horizon;
+    io->policy_action = (const R*)ra->policy_action; io->policy_ready = ra->policy_ready;
+    io->request_env = ra->request_env; io->request_noise = (R*)ra->request_noise;
+    io->request_count = ra->request_count; io->request_capacity = ra->request_capacity;
+    io->env_steps = reinterpret_cast<unsigned long long*>(ra->env_steps);
   };
   if (h->precision == SIT_F64) {
     StepIO<double> io{};
