@@ -36,19 +36,28 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=6000)
-    ap.add_argument("--warmup", type=int, default=600)
+    ap.add_argument("--steps", type=int, default=20000)
+    ap.add_argument("--warmup", type=int, default=40000, help="steps before timing (the env population "
+                    "starts synchronised; ~40k steps reach the steady state of desynchronised episodes)")
     ap.add_argument("--n-env", type=int, default=32768, help="two-ship envs per GPU (32768 = 64k ships)")
-    ap.add_argument("--chunk", type=int, default=200, help="env steps fused per kernel launch")
+    ap.add_argument("--chunk", type=int, default=None,
+                    help="env steps fused per kernel launch (default 200; 32 in policy mode)")
     ap.add_argument("--precision", type=int, default=32, choices=(32, 64))
     ap.add_argument("--seed", type=int, default=25450)
-    ap.add_argument("--mode", default="rollout", choices=("rollout", "step"),
-                    help="rollout: fused K-step launches; step: one sit_step launch per env step")
+    ap.add_argument("--mode", default="rollout", choices=("rollout", "step", "policy"),
+                    help="rollout: fused K-step launches (synthetic sampler); step: one sit_step launch "
+                         "per env step; policy: Gaussian-policy actor between launches (config C5)")
+    ap.add_argument("--groups", type=int, default=2, help="policy mode: env groups on separate streams")
+    ap.add_argument("--request-div", type=int, default=4, help="policy mode: request capacity = envs / this")
+    ap.add_argument("--graph-launches", type=int, default=16, help="policy mode: launches per HIP graph")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--launch-trace", action="store_true", help="print every launch's kernel ms to stderr")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.chunk is None:
+        args.chunk = 32 if args.mode == "policy" else 200
+    return args
 
 
 def algorithmic_bytes_per_launch(n_env, k, rs, mean_nw_obs, mean_nw_test, mode):
@@ -99,45 +108,12 @@ def cpu_baseline(seconds, seed):
                       f"sampler, auto-reset), {dt:.1f} s on 1 host core"}
 
 
-class TransitionGather:
-    """Per chunk: compact sampling-event transitions (state, action a, reward, next_state, mask)
-    on device and all-gather them over RCCL (fixed-capacity records)."""
-
-    def __init__(self, n_env, chunk, dtype, device, world, enabled):
-        self.world, self.enabled = world, enabled and world > 1
-        self.cap = max(1024, n_env * chunk // 64)
-        self.rec = torch.zeros((self.cap, 24), dtype=dtype, device=device)
-        self.gathered = torch.empty((world, self.cap, 24), dtype=dtype, device=device) if self.enabled else None
-        self.prev = None
-        self.count = torch.zeros(1, dtype=torch.int64, device=device)
-        self.total = 0
-
-    def __call__(self, out, initial_state):
-        ns = out["next_state"]
-        if self.prev is None:
-            self.prev = initial_state.clone()
-        state = torch.cat([self.prev[None], ns[:-1]], 0)
-        sel = out["action"][..., 3] > 0.5
-        idx = sel.nonzero(as_tuple=False)
-        k = min(idx.shape[0], self.cap)
-        idx = idx[:k]
-        t, e = idx[:, 0], idx[:, 1]
-        r = self.rec
-        r[:k, 0:10] = state[t, e]
-        r[:k, 10] = out["action"][t, e, 2]
-        r[:k, 11] = out["reward"][t, e]
-        r[:k, 12:22] = ns[t, e]
-        r[:k, 22] = 1.0 - out["done"][t, e].to(r.dtype)
-        r[:k, 23] = float(k)
-        self.prev = ns[-1]
-        self.total += k
-        if self.enabled:
-            import torch.distributed as dist
-            dist.all_gather_into_tensor(self.gathered, r)
+def stats_of(launch_ms):
+    v = np.asarray(launch_ms, dtype=np.float64)
+    return {"min": float(v.min()), "median": float(np.median(v)), "max": float(v.max())}
 
 
-def main():
-    args = parse()
+def setup_dist():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -146,65 +122,16 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
-    from sac_maritime_ast_amd import VecMultiShipRLEnv, make_scenario
+    return rank, world, dev
 
-    n_env = args.n_env
-    sc = make_scenario(n_env, cap=48, seed=args.seed + rank)
-    env = VecMultiShipRLEnv(scenario=sc, precision=args.precision, device=dev)
-    init_obs = env.reset()
-    env.init_step()
-    chunk = args.chunk if args.mode == "rollout" else 1
-    steps = (args.steps // chunk) * chunk
-    warm = max(chunk, (args.warmup // chunk) * chunk)
-    offset = rank * n_env
-    out = {}
-    gather = TransitionGather(n_env, chunk, env.dtype, dev, world, not args.no_gather)
-    stream = torch.cuda.current_stream(dev)
 
-    # per-step mode: precomputed random IW actions (explicit inputs), one launch per env step
-    if args.mode == "step":
-        g = torch.Generator(device=dev).manual_seed(args.seed)
-        st = env.get_state()
-        step_act = torch.stack([st["north"][1], st["east"][1]], 1) + torch.randn(n_env, 2, device=dev,
-                                                                                dtype=env.dtype, generator=g) * 500
-        step_sac = (torch.rand(n_env, device=dev, generator=g) < 0.005).to(torch.uint8)
-        step_init = torch.zeros(n_env, dtype=torch.uint8, device=dev)
-        ns = torch.empty((n_env, 10), dtype=env.dtype, device=dev)
-        rew = torch.empty((n_env,), dtype=env.dtype, device=dev)
-        done = torch.empty((n_env,), dtype=torch.uint8, device=dev)
-        stat = torch.empty((n_env,), dtype=torch.int32, device=dev)
-        dcount = torch.zeros(1, dtype=torch.int32, device=dev)
-
-        def one(i):
-            env._call("sit_step", step_act.data_ptr(), step_sac.data_ptr(), step_init.data_ptr(),
-                      ns.data_ptr(), rew.data_ptr(), done.data_ptr(), stat.data_ptr(), dcount.data_ptr(),
-                      env._stream())
-    else:
-        def one(i):
-            env.rollout(chunk, seed=args.seed, env_id_offset=offset, out=out)
-            if gather.enabled:
-                gather(out, init_obs)
-
-    for i in range(warm // chunk):
-        one(i)
+def timed(dev, world, fn):
+    """Barrier + synchronize on both sides of fn(); max over ranks of the wall time."""
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
-    n_launch = steps // chunk
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
-    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(n_launch):
-        if args.mode == "rollout":
-            ev[i][0].record(stream)
-            env.rollout(chunk, seed=args.seed, env_id_offset=offset, out=out)
-            ev[i][1].record(stream)
-            if gather.enabled:
-                gather(out, init_obs)
-        else:
-            ev[i][0].record(stream)
-            one(i)
-            ev[i][1].record(stream)
+    fn()
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -212,45 +139,182 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    elapsed = float(t.item())
+    return float(t.item())
+
+
+def roofline(alg_bytes, kern_ms, pmc):
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": (pmc["hbm_bytes_per_launch"] if pmc else None),
+            "kernel": "k_env_steps", "kernel_ms_per_launch": kern_ms,
+            "algorithmic_bytes_per_launch": alg_bytes}
+
+
+def bench_rollout(args, rank, world, dev):
+    """Configs C3/C4: synthetic random-IW sampler on device, fused `chunk`-step launches."""
+    from sac_maritime_ast_amd import VecMultiShipRLEnv, make_scenario
+    from sac_maritime_ast_amd.shard import TransitionGather, shard_offset
+
+    n_env = args.n_env
+    offset = shard_offset(rank, n_env)
+    sc = make_scenario(n_env, cap=48, seed=args.seed, env_offset=offset)
+    env = VecMultiShipRLEnv(scenario=sc, precision=args.precision, device=dev)
+    env.reset()
+    env.init_step()
+    chunk = args.chunk if args.mode == "rollout" else 1
+    steps = max(chunk, (args.steps // chunk) * chunk)
+    warm = max(chunk, (args.warmup // chunk) * chunk)
+    stream = torch.cuda.current_stream(dev)
+    # replay transitions of sampling events: written by the kernel with a device-side count and
+    # all-gathered over RCCL once per launch (no host synchronisation)
+    tcap = max(1024, n_env * chunk // 64)
+    gather = TransitionGather(tcap, 24, env.dtype, dev, world) if (world > 1 and not args.no_gather) else None
+    out = {}
+
+    if args.mode == "step":   # one sit_step launch per env step, explicit (precomputed) random IWs
+        g = torch.Generator(device=dev).manual_seed(args.seed)
+        st = env.get_state()
+        act = torch.stack([st["north"][1], st["east"][1]], 1) + torch.randn(n_env, 2, device=dev, dtype=env.dtype,
+                                                                           generator=g) * 500
+        sac = (torch.rand(n_env, device=dev, generator=g) < 0.005).to(torch.uint8)
+        init = torch.zeros(n_env, dtype=torch.uint8, device=dev)
+        bufs = [torch.empty((n_env, 10), dtype=env.dtype, device=dev), torch.empty(n_env, dtype=env.dtype, device=dev),
+                torch.empty(n_env, dtype=torch.uint8, device=dev), torch.empty(n_env, dtype=torch.int32, device=dev),
+                torch.zeros(1, dtype=torch.int32, device=dev)]
+
+        def one():
+            env._call("sit_step", act.data_ptr(), sac.data_ptr(), init.data_ptr(), *[b.data_ptr() for b in bufs],
+                      env._stream())
+    else:
+        def one():
+            env.rollout(chunk, seed=args.seed, env_id_offset=offset, out=out,
+                        transition_capacity=tcap if gather else 0)
+            if gather:
+                gather(out["transitions"], out["transition_count"])
+
+    for _ in range(warm // chunk):
+        one()
+    n_launch = steps // chunk
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
+
+    def run():
+        for i in range(n_launch):
+            ev[i][0].record(stream)
+            one()
+            ev[i][1].record(stream)
+    elapsed = timed(dev, world, run)
     launch_ms = [a.elapsed_time(b) for a, b in ev]
-    kern_ms = float(np.mean(launch_ms))
     if args.launch_trace:
         print("launch_ms " + " ".join(f"{x:.4f}" for x in launch_ms), file=sys.stderr)
-
+    kern_ms = float(np.mean(launch_ms))
     st = env.get_state()
-    mean_nw_obs = float(st["n_wpt"][1].double().mean().item())
-    mean_nw_test = float(st["n_wpt"][0].double().mean().item())
     rs = 4 if args.precision == 32 else 8
-    alg = algorithmic_bytes_per_launch(n_env, chunk, rs, mean_nw_obs, mean_nw_test, args.mode)
-    achieved = alg / (kern_ms * 1e-3) / 1e9
-    pmc = latest_pmc(args.precision, args.mode)
+    alg = algorithmic_bytes_per_launch(n_env, chunk, rs, float(st["n_wpt"][1].double().mean().item()),
+                                       float(st["n_wpt"][0].double().mean().item()), args.mode)
     env_steps = world * n_env * steps
-    result = {
-        "metric": METRIC,
-        "value": env_steps / elapsed,
-        "unit": "env-steps/s",
-        "n_gpus": world,
-        "steps": steps,
-        "warmup": warm,
-        "ms_per_step": elapsed * 1e3 / steps,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32" if args.precision == 32 else "f64",
-        "data": "synthetic (SURVEY §8(d) routes, island map of test_policy.py:189-194, Philox random IWs)",
-        "config": {"workload": "C3: 65 536 ships = 32 768 two-ship envs per GPU, random IW actions, auto-reset",
-                   "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env, "fused_steps_per_launch": chunk,
-                   "mode": args.mode, "parallelism": f"env-shard x{world}",
-                   "ship_steps_per_s": 2 * env_steps / elapsed,
-                   "rccl_transition_gather": bool(gather.enabled), "transitions_compacted": gather.total},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": (pmc["hbm_bytes_per_launch"] if pmc else None),
-                     "kernel": "k_env_steps", "kernel_ms_per_launch": kern_ms,
-                     "algorithmic_bytes_per_launch": alg,
-                     "algorithmic_bytes_per_env_step": alg / (n_env * chunk)},
+    rl = roofline(alg, kern_ms, latest_pmc(args.precision, args.mode))
+    rl["algorithmic_bytes_per_env_step"] = alg / (n_env * chunk)
+    rl["launch_ms"] = stats_of(launch_ms)
+    workload = ("C3: 65 536 ships = 32 768 two-ship envs per GPU, random IW actions, auto-reset" if world == 1 else
+                f"C4: {2 * n_env * world} ships sharded over {world} GPUs, random IW actions, RCCL transition gather")
+    return {
+        "value": env_steps / elapsed, "steps": steps, "warmup": warm, "ms_per_step": elapsed * 1e3 / steps,
+        "config": {"workload": workload, "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env,
+                   "fused_steps_per_launch": chunk, "mode": args.mode, "parallelism": f"env-shard x{world}",
+                   "ship_steps_per_s": 2 * env_steps / elapsed, "rccl_transition_gather": gather is not None},
+        "roofline": rl,
     }
+
+
+def bench_policy(args, rank, world, dev):
+    """Config C5: the SAC-AST Gaussian policy (PyTorch-ROCm fp32 actor, 256x256 MLP) chooses the
+    IWs; envs split into `--groups` groups on separate HIP streams so one group's actor runs while
+    the others' env kernels run.  value = env-steps executed (device counter) / time."""
+    from sac_maritime_ast_amd import VecMultiShipRLEnv, make_scenario
+    from sac_maritime_ast_amd.samplers import GaussianPolicy, PolicySampler
+    from sac_maritime_ast_amd.shard import shard_offset
+
+    n_env, G, chunk = args.n_env, args.groups, args.chunk
+    per = n_env // G
+    torch.manual_seed(args.seed)
+    policy = GaussianPolicy(hidden=(256, 256)).to(dev)
+    samplers = []
+    for g in range(G):
+        off = shard_offset(rank, n_env) + g * per
+        env = VecMultiShipRLEnv(scenario=make_scenario(per, cap=48, seed=args.seed, env_offset=off),
+                                precision=args.precision, device=dev)
+        env.reset()
+        env.init_step()
+        samplers.append(PolicySampler(env, policy, chunk=chunk, seed=args.seed, env_id_offset=off,
+                                      request_capacity=max(256, per // args.request_div)))
+    from sac_maritime_ast_amd.samplers import OverlappedPolicySampler
+    runner = OverlappedPolicySampler(samplers) if G > 1 else samplers[0]
+    cur = torch.cuda.current_stream(dev)
+    # kernel duration of the env launches (eager, HIP events on each group's stream)
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
+          for _ in range(8)]
+    for i in range(8):
+        for g, sm in enumerate(samplers):
+            st = runner.streams[g] if G > 1 else cur
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                sm.io["request_count"].zero_()
+                ev[i][g][0].record(st)
+                sm.env.rollout(chunk, seed=args.seed, env_id_offset=sm.env_id_offset, out=sm.out, policy_io=sm.io)
+                ev[i][g][1].record(st)
+                sm.act()
+            cur.wait_stream(st)
+    torch.cuda.synchronize(dev)
+    launch_ms = [a.elapsed_time(b) for row in ev for a, b in row]
+    # the timed loop: HIP-graph replays of `per_graph` launches of every group
+    per_graph = max(1, min(args.graph_launches, args.steps // chunk))
+    runner.capture(per_graph)
+    n_rep = max(1, args.steps // (chunk * per_graph))
+    n_warm = max(1, args.warmup // (chunk * per_graph))
+    for _ in range(n_warm):
+        runner.replay()
+    torch.cuda.synchronize(dev)
+    before = sum(int(sm.env_steps.item()) for sm in samplers)
+
+    def run():
+        for _ in range(n_rep):
+            runner.replay()
+    elapsed = timed(dev, world, run)
+    n_launch = n_rep * per_graph
+    done_steps = sum(int(sm.env_steps.item()) for sm in samplers) - before
+    tot = torch.tensor([done_steps], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(tot)
+    env_steps = float(tot.item())
+    kern_ms = float(np.mean(launch_ms))
+    rs = 4 if args.precision == 32 else 8
+    alg = algorithmic_bytes_per_launch(per, chunk, rs, 3.0, 5.0, "rollout")
+    rl = roofline(alg, kern_ms, None)
+    rl["launch_ms"] = stats_of(launch_ms)
+    rl["note"] = "per group launch (n_env / groups envs), groups run concurrently on separate streams"
+    return {
+        "value": env_steps / elapsed, "steps": n_launch * chunk, "warmup": n_warm * per_graph * chunk,
+        "ms_per_step": elapsed * 1e3 / (n_launch * chunk),
+        "config": {"workload": "C5: 65 536 ships driven by the SAC-AST Gaussian policy (256x256 MLP, PyTorch-ROCm "
+                               "fp32 actor) interleaved with the HIP env step on separate streams",
+                   "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env, "fused_steps_per_launch": chunk,
+                   "mode": "policy", "stream_groups": G, "launches_per_hip_graph": per_graph,
+                   "parallelism": f"env-shard x{world}",
+                   "env_step_fraction": env_steps / (world * n_env * n_launch * chunk),
+                   "policy_evaluations": int(sum(int(sm.served.item()) for sm in samplers))},
+        "roofline": rl,
+    }
+
+
+def main():
+    args = parse()
+    rank, world, dev = setup_dist()
+    r = bench_policy(args, rank, world, dev) if args.mode == "policy" else bench_rollout(args, rank, world, dev)
+    result = {"metric": METRIC, "value": r["value"], "unit": "env-steps/s", "n_gpus": world, "steps": r["steps"],
+              "warmup": r["warmup"], "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+              "vs_baseline": None, "dtype": "f32" if args.precision == 32 else "f64",
+              "data": "synthetic (SURVEY §8(d) routes, island map of test_policy.py:189-194, Philox random IWs)",
+              "config": r["config"], "roofline": r["roofline"]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.seed)
     if rank == 0:

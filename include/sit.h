@@ -295,6 +295,7 @@ typedef struct sit_rollout_args {
   int32_t* policy_ready;      /* int32[n_env] */
   int32_t* request_env;       /* int32[request_capacity] */
   void* request_noise;        /* real[request_capacity] */
+  void* request_obs;          /* real[request_capacity][SIT_OBS_DIM]: the waiting env's state */
   int32_t* request_count;     /* int32[1] */
   int32_t request_capacity;
   int64_t* env_steps;         /* int64[1] or NULL: += env-steps executed (policy mode) */

@@ -279,6 +279,25 @@ def sampler_uniform(seed, env_id, event):
     return (hi * 67108864.0 + lo) * (1.0 / 9007199254740992.0)
 
 
+POLICY_TAG = 0x504F
+
+
+def sampler_normal(seed, env_id, event):
+    """Standard normal from Philox(key=seed, ctr=(env_id, event, 0x504F, 0)) by Box-Muller:
+    u1 in (0, 1], u2 in [0, 1) from 53 bits each (the policy's reparameterisation noise)."""
+    env_id = np.asarray(env_id, dtype=np.uint64)
+    event = np.asarray(event, dtype=np.uint64)
+    seed = int(seed)
+    key = (np.uint64(seed & _MASK), np.uint64((seed >> 32) & _MASK))
+    x = philox4x32_10((env_id & np.uint64(_MASK), event & np.uint64(_MASK),
+                       np.uint64(POLICY_TAG), np.uint64(0)), key)
+    u1 = ((x[0] >> np.uint32(5)).astype(np.float64) * 67108864.0
+          + (x[1] >> np.uint32(6)).astype(np.float64) + 1.0) * (1.0 / 9007199254740992.0)
+    u2 = ((x[2] >> np.uint32(5)).astype(np.float64) * 67108864.0
+          + (x[3] >> np.uint32(6)).astype(np.float64)) * (1.0 / 9007199254740992.0)
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+
+
 # ------------------------------------------------------------------------------------
 # the env
 # ------------------------------------------------------------------------------------
@@ -721,6 +740,44 @@ class OracleEnvs:
         s["event"] = np.where(sample, s["event"] + 1, s["event"])
         act = np.stack([s["iw_north"], s["iw_east"]], axis=1)
         return act, sample, init, np.where(sample, a, np.nan)
+
+    def policy_rollout(self, n_steps, seed, policy, env_id_offset=0):
+        """The synchronous loop of test_beds/main_ast.py:310-412 with a policy choosing the IW
+        (agent.select_action mode 1, :344-349): at every sampling event (episode start, or the
+        sampling distance reaching AB_len while the obstacle ship runs) policy(state[m, 10],
+        noise[m]) -> action[m] in [-1, 1] with noise = sampler_normal(seed, env_id, event); the
+        route angle is a = action * pi / 6 and IW = obstacle position + AB_len (cos, sin)(AB_alpha
+        + a).  Auto-reset on done.  Returns dict of [K, n_env, ...] arrays (action rows hold IW
+        north, IW east, a, SAC_update) and the per-event policy actions."""
+        s = self.s
+        out = dict(next_state=[], reward=[], done=[], status=[], action=[])
+        env_id = np.arange(self.n_env, dtype=np.uint64) + np.uint64(env_id_offset)
+        for _ in range(n_steps):
+            init = s["ep_step"] == 0
+            stopped = s["stop"][1].astype(bool)
+            sample = init | ((s["sampling_dist"] >= self.ab_len) & ~stopped)
+            ang = np.full(self.n_env, np.nan)
+            idx = np.nonzero(sample)[0]
+            if idx.size:
+                state = self.s["last_obs"].T[idx]
+                noise = sampler_normal(seed, env_id[idx], s["event"][idx])
+                a = np.asarray(policy(state, noise), dtype=np.float64).reshape(-1)
+                ang[idx] = a * (np.pi / 6.0)
+                s["iw_north"][idx] = s["north"][1][idx] + self.ab_len[idx] * np.cos(self.ab_alpha[idx] + ang[idx])
+                s["iw_east"][idx] = s["east"][1][idx] + self.ab_len[idx] * np.sin(self.ab_alpha[idx] + ang[idx])
+                s["event"][idx] = s["event"][idx] + 1
+            act = np.stack([s["iw_north"], s["iw_east"]], axis=1)
+            ns, rew, done, st = self.step(act, sample, init)
+            out["next_state"].append(ns)
+            out["reward"].append(rew)
+            out["done"].append(done)
+            out["status"].append(st)
+            out["action"].append(np.stack([act[:, 0], act[:, 1], ang, sample.astype(float)], axis=1))
+            if done.any():
+                self.reset(done)
+                self.s["episodes"] = self.s["episodes"] + done.astype(np.int64)
+                self.init_step(done)
+        return {k: np.stack(v) for k, v in out.items()}
 
     def rollout(self, n_steps, seed, auto_reset=True, env_id_offset=0, actions=None, mask_horizon=600):
         """K steps of the test_beds/main_ast.py:310-412 loop: reset+init_step on done, synthetic

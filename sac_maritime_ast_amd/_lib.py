@@ -75,7 +75,8 @@ class RolloutArgs(ctypes.Structure):
         ("transitions", c_void_p), ("transition_count", c_void_p), ("transition_capacity", c_int32),
         ("mask_horizon", c_int32),
         ("policy_action", c_void_p), ("policy_ready", c_void_p), ("request_env", c_void_p),
-        ("request_noise", c_void_p), ("request_count", c_void_p), ("request_capacity", c_int32),
+        ("request_noise", c_void_p), ("request_obs", c_void_p), ("request_count", c_void_p),
+        ("request_capacity", c_int32),
         ("env_steps", c_void_p),
     ]
 

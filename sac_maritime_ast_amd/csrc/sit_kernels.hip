@@ -118,6 +118,7 @@ struct StepIO {
   int32_t* policy_ready;
   int32_t* request_env;
   T* request_noise;
+  T* request_obs;
   int32_t* request_count;
   int32_t request_capacity;
   unsigned long long* env_steps;
@@ -422,15 +423,19 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #endif
     bool sac = false, init_f = false;
     double ang = NAN;
+    bool stall_now = false;
     if (MODE == kPolicy && act && !stalled && need && !ready) {
       // sampling event without an action: wait for the policy; the obstacle lane queues the
       // request with this event's standard-normal draw (reparameterised sample, normal.py:96-101)
-      stalled = true;
+      // and its half of the observation; the test lane adds its half after the exchange
+      stalled = stall_now = true;
       if (type == 1) {
         const int q = atomicAdd(a.io.request_count, 1);
+        x.slot[lane] = q;
         if (q < a.io.request_capacity) {
           a.io.request_env[q] = env;
           a.io.request_noise[q] = (T)sampler_normal(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
+          for (int j = 0; j < 4; ++j) a.io.request_obs[(size_t)q * SIT_OBS_DIM + 6 + j] = lo[j];
         }
       }
     }
@@ -580,7 +585,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       x.n[type][lane] = s.n;
       x.e[type][lane] = s.e;
       x.bits[type][lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u) |
-                           ((type == 1 && (double)samp >= ab_len) ? kSampGeBit : 0u);
+                           ((MODE == kPolicy && type == 1 && (double)samp >= ab_len) ? kSampGeBit : 0u);
       if (type == 1) { x.r_nto[lane] = r_nt; x.r_o[lane] = r_term; }
     }
     SIT_PH(3);
@@ -594,6 +599,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     if (MODE == kPolicy && act && !live && type == 0) {   // no step taken this row
       if (a.io.status) a.io.status[row] = SIT_ST_NO_STEP;
       if (a.io.done) a.io.done[row] = 0;
+      if (stall_now) {
+        const int q = x.slot[lane];
+        if (q < a.io.request_capacity)
+          for (int j = 0; j < 6; ++j) a.io.request_obs[(size_t)q * SIT_OBS_DIM + j] = lo[j];
+      }
     }
     if (live) {
       const T dn = x.n[0][lane] - x.n[1][lane], de = x.e[0][lane] - x.e[1][lane];
@@ -605,7 +615,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         const T r_snt = (bo & kStopBit) ? T(0) : (T(1) - xsqrt(dn * dn + de * de) * c.inv_maxn) * T(0.001);
         const T rs = coll ? T(2000) : T(0);
         const T reward = r_nt + r_term + x.r_nto[lane] + x.r_o[lane] + r_snt + rs;
-        const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
+        const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit | kSampGeBit)) | (coll ? SIT_ST_COLLISION : 0u);
 #ifndef SIT_ABLATE_STORES
         if (a.io.reward) a.io.reward[row] = reward;
         if (a.io.done) a.io.done[row] = env_done ? 1 : 0;
@@ -655,7 +665,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       if (type == 0) { lo[0] = s.n; lo[1] = s.e; lo[2] = s.psi; lo[3] = o_rpm; lo[4] = o_ect; lo[5] = o_pme; }
       else { lo[0] = s.n; lo[1] = s.e; lo[2] = s.psi; lo[3] = o_ect; }
       if (MODE == kPolicy) {
-        if (sac) ready = false;        // the action was consumed
+        if (need) ready = false;       // this step's sampling event consumed the action (both lanes)
         // the next step is a sampling event at an episode start or once the sampling distance
         // reaches AB_len while the obstacle ship runs (the obstacle lane's own test, exchanged)
         const bool obs_stop = (bo & kStopBit) || coll;
@@ -855,6 +865,7 @@ struct sit_handle {
   size_t map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0, map_frank = 0, map_crec = 0, map_clive = 0;
   int use_cells = 0;
   int64_t n_mixed = 0, n_live = 0;
+  int lds_attr[6] = {-1, -1, -1, -1, -1, -1};   // dynamic-LDS size set per step-kernel variant
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
@@ -1043,7 +1054,13 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   const bool lds_map = map_lds_bytes(h) + stat <= kLdsBudget;
   const size_t lds = lds_map ? map_lds_bytes(h) : 0;
   auto go = [&](auto kern) -> int {
-    if (lds_map) HIP_TRY(h, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    // the dynamic-LDS attribute is set once per kernel and size (not per launch: launches may be
+    // captured into HIP graphs)
+    const int slot = mode * 2 + (lds_map ? 1 : 0);
+    if (lds_map && h->lds_attr[slot] != (int)lds) {
+      HIP_TRY(h, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      h->lds_attr[slot] = (int)lds;
+    }
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(128), lds, stream, a);
     return SIT_OK;
   };
@@ -1646,10 +1663,10 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     return fail(h, SIT_E_INVALID, "transitions need transition_count and a positive capacity");
   if (ra->policy_action && ra->action_ne)
     return fail(h, SIT_E_INVALID, "policy mode and explicit actions are exclusive");
-  if (ra->policy_action && (!ra->policy_ready || !ra->request_env || !ra->request_noise ||
+  if (ra->policy_action && (!ra->policy_ready || !ra->request_env || !ra->request_noise || !ra->request_obs ||
                             !ra->request_count || ra->request_capacity <= 0))
     return fail(h, SIT_E_INVALID, "policy mode needs policy_ready, request_env, request_noise, "
-                                  "request_count and a positive request_capacity");
+                                  "request_obs, request_count and a positive request_capacity");
   auto fill = [&](auto* io, auto* tag) {
     using R = std::remove_pointer_t<decltype(tag)>;
     io->n_steps = ra->n_steps; io->auto_reset = ra->auto_reset; io->seed = ra->seed;
@@ -1661,6 +1678,7 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     io->transition_capacity = ra->transition_capacity; io->mask_horizon = ra->mask_horizon;
     io->policy_action = (const R*)ra->policy_action; io->policy_ready = ra->policy_ready;
     io->request_env = ra->request_env; io->request_noise = (R*)ra->request_noise;
+    io->request_obs = (R*)ra->request_obs;
     io->request_count = ra->request_count; io->request_capacity = ra->request_capacity;
     io->env_steps = reinterpret_cast<unsigned long long*>(ra->env_steps);
   };

@@ -171,11 +171,13 @@ class VecMultiShipRLEnv:
     def rollout(self, n_steps: int, seed: int = 25450, auto_reset: bool = True, env_id_offset: int = 0,
                 actions: dict | None = None, out: dict | None = None, want=("next_state", "reward", "done",
                                                                               "status", "action", "done_count"),
-                transition_capacity: int = 0, mask_horizon: int = 600):
+                transition_capacity: int = 0, mask_horizon: int = 600, policy_io: dict | None = None):
         """K fused steps (one kernel launch).  actions=None: synthetic AST sampler on device.
         Returns a dict of [K, n_env, ...] tensors (reused from `out` when given).  With
         transition_capacity > 0 the sampling-event replay transitions are appended to
-        out["transitions"] ([capacity, 24]) and counted in out["transition_count"] ([1])."""
+        out["transitions"] ([capacity, 24]) and counted in out["transition_count"] ([1]).
+        policy_io: the policy-mode buffers (see samplers.PolicySampler): actions of sampling events
+        come from a policy run between launches; waiting envs' rows carry status ST_NO_STEP."""
         n, K = self.n_env, int(n_steps)
         out = {} if out is None else out
         shapes = {"next_state": ((K, n, _lib.SIT_OBS_DIM), self.dtype), "reward": ((K, n), self.dtype),
@@ -213,6 +215,13 @@ class VecMultiShipRLEnv:
             ra.transition_count = out["transition_count"].data_ptr()
             ra.transition_capacity = int(transition_capacity)
         ra.mask_horizon = int(mask_horizon)
+        if policy_io is not None:
+            if actions is not None:
+                raise ValueError("policy mode and explicit actions are exclusive")
+            for k in ("policy_action", "policy_ready", "request_env", "request_noise", "request_obs",
+                      "request_count", "env_steps"):
+                setattr(ra, k, policy_io[k].data_ptr())
+            ra.request_capacity = int(policy_io["request_env"].numel())
         with torch.cuda.device(self.device):
             _lib.check(self.lib.sit_rollout(self.handle, byref(ra), self._stream()), self.handle)
         return out

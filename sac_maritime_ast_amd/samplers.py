@@ -1,0 +1,214 @@
+"""Build-owned AST samplers: the counterpart of the reference's (empty)
+``ast_core/samplers/intermediate_waypoint_sampler.py`` and of the episode loop of
+``test_beds/main_ast.py:310-412``, driving the HIP env step.
+
+Two action sources, as in ``agent.select_action(state, done, init, mode)`` (main_ast.py:337-349):
+
+* mode 0 (``start_steps``, random sampling): the route scoping angle a ~ U[-pi/6, pi/6] drawn on
+  device (the synthetic sampler of ``sit_rollout``; ``UniformPolicy``, uniform_policy.py:18-21,
+  gives actions U[-1, 1], scaled by the action bound pi/6).
+* mode 1 (policy sampling): the SAC actor, a squashed Gaussian MLP (``GaussianPolicy`` below),
+  evaluated in PyTorch-ROCm between fused K-step launches of the env kernel.
+
+Policy mode on the GPU: an env whose next step is a sampling event and that holds no fresh
+action stops for the rest of the launch and queues a request (its observation and a
+standard-normal draw keyed by (seed, env id, event)); after the launch the actor runs on the
+queued observations and scatters the squashed actions into per-env slots; the next launch
+consumes them.  Each env's trajectory is the one the synchronous per-step loop produces
+(oracle/sit_oracle.py ``OracleEnvs.policy_rollout``; tests/test_gpu_policy.py), independent of
+how envs are batched into launches.  ``OverlappedPolicySampler`` splits the envs into groups
+on separate HIP streams so one group's actor runs while the others' env kernels run.
+
+The converter from action to simulator input (``agent.convert_action_to_simu_input``) is absent
+from the reference; the build defines it: route angle a = action * pi/6 and
+IW = obstacle position + AB_len (cos, sin)(AB_alpha + a), inserted at index -1 of the obstacle
+ship's route with SAC_update on sampling events only.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from . import _lib
+from .env import VecMultiShipRLEnv
+
+LOG_SIG_CAP_MIN, LOG_SIG_CAP_MAX = -20.0, 2.0   # ast_core/distributions/normal.py:15-16
+EPS = 1e-6                                      # ast_core/policies/gaussian_policy.py:18
+
+
+class GaussianPolicy(nn.Module):
+    """Squashed Gaussian policy: ast_core/policies/gaussian_policy.py:19-148 with the Normal head of
+    ast_core/distributions/normal.py:17-133 and the MLP of ast_core/nn_models/mlp.py:95-148.
+
+    obs [N, obs_dim] -> ReLU hidden layers -> [mu, log_sigma] ([N, 2*Da], no output nonlinearity);
+    log_sigma clipped to [-20, 2]; x = mu + exp(log_sigma) * noise (reparameterised sample,
+    normal.py:96-101); action = tanh(x) (squash=True); log_pi = sum_d log N(x_d; mu_d, sigma_d)
+    - sum_d log(1 - tanh(x_d)^2 + 1e-6) (gaussian_policy.py:88-94, 141-144).  The reference's
+    TF1 graph (tensorflow/tfp/rllab) is not importable here: parity of this head is pinned to its
+    formulas (tests/test_samplers.py), not to a reference run.  Hidden size 256 x 2 is
+    main_ast.py:67's default."""
+
+    def __init__(self, obs_dim: int = _lib.SIT_OBS_DIM, act_dim: int = 1, hidden=(256, 256)):
+        super().__init__()
+        layers, d = [], obs_dim
+        for h in hidden:
+            layers += [nn.Linear(d, h), nn.ReLU()]
+            d = h
+        layers.append(nn.Linear(d, 2 * act_dim))
+        self.net = nn.Sequential(*layers)
+        self.act_dim = act_dim
+
+    def forward(self, obs: torch.Tensor, noise: torch.Tensor | None = None, deterministic: bool = False):
+        out = self.net(obs)
+        mu, log_sig = out[..., :self.act_dim], out[..., self.act_dim:]
+        log_sig = log_sig.clamp(LOG_SIG_CAP_MIN, LOG_SIG_CAP_MAX)
+        if deterministic:                     # GaussianPolicy.get_actions, _is_deterministic (:114-126)
+            x = mu
+        else:
+            if noise is None:
+                noise = torch.randn_like(mu)
+            x = mu + log_sig.exp() * noise.reshape(mu.shape)
+        action = torch.tanh(x)
+        sig = log_sig.exp()
+        log_prob = (-0.5 * ((x - mu) / sig) ** 2 - log_sig - 0.5 * math.log(2 * math.pi)).sum(-1)
+        log_pi = log_prob - torch.log(1 - action ** 2 + EPS).sum(-1)
+        return action, log_pi, mu, log_sig
+
+
+class PolicySampler:
+    """Fused K-step launches in policy mode with the actor evaluated between launches.
+
+    request_capacity bounds the envs served per launch (default n_env: every waiting env);
+    envs beyond it keep waiting and re-request on the next launch.  The actor runs on a fixed
+    number of rows (no host synchronisation); rows past the device-side request count are
+    scattered into a dummy slot."""
+
+    def __init__(self, env: VecMultiShipRLEnv, policy: nn.Module, chunk: int = 32, seed: int = 25450,
+                 env_id_offset: int = 0, request_capacity: int | None = None, mask_horizon: int = 600,
+                 transition_capacity: int = 0, deterministic: bool = False, actor_dtype=None):
+        self.env, self.policy, self.chunk, self.seed = env, policy, int(chunk), int(seed)
+        self.env_id_offset, self.mask_horizon = int(env_id_offset), int(mask_horizon)
+        self.transition_capacity, self.deterministic = int(transition_capacity), deterministic
+        n, dev, dt = env.n_env, env.device, env.dtype
+        cap = int(request_capacity or n)
+        self.actor_dtype = actor_dtype or next(policy.parameters()).dtype
+        self.io = {
+            "policy_action": torch.zeros(n + 1, dtype=dt, device=dev),      # slot n: dummy
+            "policy_ready": torch.zeros(n + 1, dtype=torch.int32, device=dev),
+            "request_env": torch.zeros(cap, dtype=torch.int32, device=dev),
+            "request_noise": torch.zeros(cap, dtype=dt, device=dev),
+            "request_obs": torch.zeros((cap, _lib.SIT_OBS_DIM), dtype=dt, device=dev),
+            "request_count": torch.zeros(1, dtype=torch.int32, device=dev),
+            "env_steps": torch.zeros(1, dtype=torch.int64, device=dev),
+        }
+        self._rows = torch.arange(cap, device=dev, dtype=torch.int32)
+        self._one = torch.ones(cap, dtype=torch.int32, device=dev)
+        self.out: dict = {}
+        self.served = torch.zeros(1, dtype=torch.int64, device=dev)   # policy evaluations used
+
+    @property
+    def env_steps(self) -> torch.Tensor:
+        """Env-steps executed so far (device int64[1])."""
+        return self.io["env_steps"]
+
+    def launch(self, want=("next_state", "reward", "done", "status", "action")):
+        """One fused launch of `chunk` steps followed by the actor on the queued requests.
+        Returns the launch's [K, n_env, ...] outputs (rows of waiting envs: status ST_NO_STEP)."""
+        self.io["request_count"].zero_()
+        self.env.rollout(self.chunk, seed=self.seed, env_id_offset=self.env_id_offset, out=self.out,
+                         want=want, transition_capacity=self.transition_capacity,
+                         mask_horizon=self.mask_horizon, policy_io=self.io)
+        self.act()
+        return self.out
+
+    def capture(self, n_launch: int = 1, want=("next_state", "reward", "done", "status", "action")):
+        """Record `n_launch` launches (env kernel + actor) into one HIP graph; replay() then runs
+        them with a single submission (the per-launch host work of ctypes and ~10 torch ops
+        otherwise bounds short chunks).  The output buffers are those of the last launch."""
+        self.launch(want)                     # allocate every buffer outside the capture
+        torch.cuda.synchronize(self.env.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            for _ in range(n_launch):
+                self.launch(want)
+        return self
+
+    def replay(self):
+        self.graph.replay()
+        return self.out
+
+    @torch.no_grad()
+    def act(self):
+        """Actor forward on the queued observations; scatter into the per-env action slots."""
+        io, n = self.io, self.env.n_env
+        count = io["request_count"].clamp(max=self._rows.numel())
+        idx = torch.where(self._rows < count, io["request_env"], n).long()
+        obs = io["request_obs"].to(self.actor_dtype)
+        noise = io["request_noise"].to(self.actor_dtype)
+        action, _, _, _ = self.policy(obs, noise, deterministic=self.deterministic)
+        io["policy_action"].index_put_((idx,), action[:, 0].to(io["policy_action"].dtype))
+        io["policy_ready"].index_put_((idx,), self._one)
+        self.served += count.to(torch.int64)
+
+
+class OverlappedPolicySampler:
+    """Envs split into groups, each with its own HIP stream: while one group's actor runs, the
+    other groups' env kernels keep the CUs busy (BASELINE config 5)."""
+
+    def __init__(self, samplers: list[PolicySampler], device=None):
+        self.samplers = samplers
+        dev = device or samplers[0].env.device
+        self.streams = [torch.cuda.Stream(device=dev) for _ in samplers]
+
+    def launch(self, want=("next_state", "reward", "done", "status", "action")):
+        cur = torch.cuda.current_stream(self.streams[0].device)
+        outs = []
+        for sm, st in zip(self.samplers, self.streams):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                outs.append(sm.launch(want))
+        for st in self.streams:
+            cur.wait_stream(st)
+        return outs
+
+    def env_steps(self) -> torch.Tensor:
+        return sum(sm.env_steps for sm in self.samplers)
+
+    def capture(self, n_launch: int = 1, want=("next_state", "reward", "done", "status", "action")):
+        """One HIP graph holding `n_launch` rounds of every group (forked onto the groups'
+        streams inside the capture, joined at the end)."""
+        self.launch(want)
+        torch.cuda.synchronize(self.streams[0].device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            for _ in range(n_launch):
+                self.launch(want)
+        return self
+
+    def replay(self):
+        self.graph.replay()
+        return [sm.out for sm in self.samplers]
+
+
+class IntermediateWaypointSampler:
+    """The AST sampler the reference leaves empty: mode 0 (random IWs, on-device Philox draws)
+    until `start_steps` env-steps, then mode 1 (policy) — main_ast.py:337-349."""
+
+    def __init__(self, env: VecMultiShipRLEnv, policy: nn.Module | None = None, chunk: int = 32,
+                 seed: int = 25450, start_steps: int = 0, env_id_offset: int = 0, **kw):
+        self.env, self.chunk, self.seed, self.env_id_offset = env, int(chunk), int(seed), int(env_id_offset)
+        self.start_steps = int(start_steps)
+        self.total = 0
+        self.policy_sampler = PolicySampler(env, policy, chunk, seed, env_id_offset, **kw) if policy is not None else None
+        self.out: dict = {}
+
+    def launch(self):
+        if self.policy_sampler is None or self.total < self.start_steps:
+            self.env.rollout(self.chunk, seed=self.seed, env_id_offset=self.env_id_offset, out=self.out)
+            self.total += self.chunk * self.env.n_env
+            return self.out
+        out = self.policy_sampler.launch()
+        self.total += self.chunk * self.env.n_env
+        return out

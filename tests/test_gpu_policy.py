@@ -1,0 +1,152 @@
+"""GPU parity of the policy-driven sampler (config 5 path) against the oracle's synchronous loop.
+
+The HIP kernel's policy mode lets an env wait (rows with status ST_NO_STEP) until the actor has
+produced the action of its sampling event; the oracle (OracleEnvs.policy_rollout) runs the
+reference's per-step loop (test_beds/main_ast.py:310-412, agent.select_action mode 1) with the
+same policy and the same Philox noise.  Per env, the k-th executed GPU step must equal the
+oracle's k-th step: float64 within 1e-9 (per-field floors), discrete outputs identical.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import OBS_SCALE
+from oracle import sit_oracle as so
+
+pytestmark = pytest.mark.gpu
+
+sit = pytest.importorskip("sac_maritime_ast_amd")
+from sac_maritime_ast_amd import VecMultiShipRLEnv, _lib, make_scenario  # noqa: E402
+from sac_maritime_ast_amd.samplers import (GaussianPolicy, OverlappedPolicySampler,  # noqa: E402
+                                           PolicySampler)
+
+DEV = "cuda:0"
+SEED = 4242
+
+
+def make_policy(dtype, device):
+    torch.manual_seed(3)
+    pol = GaussianPolicy(hidden=(64, 64))
+    with torch.no_grad():   # make the actor's actions span [-1, 1] on this state scale
+        pol.net[0].weight.mul_(1e-3)
+    return pol.to(dtype=dtype, device=device)
+
+
+def oracle_policy_fn(pol_cpu):
+    def fn(state, noise):
+        with torch.no_grad():
+            a, _, _, _ = pol_cpu(torch.from_numpy(state), torch.from_numpy(np.asarray(noise)))
+        return a[:, 0].numpy()
+    return fn
+
+
+def run_gpu(sampler_list, n_launch):
+    """Per env, the executed rows in order: dict of lists of numpy arrays."""
+    rows = []
+    for _ in range(n_launch):
+        outs = sampler_list.launch() if hasattr(sampler_list, "samplers") else [sampler_list.launch()]
+        torch.cuda.synchronize()
+        rows.append([{k: v.cpu().numpy().copy() for k, v in o.items() if k != "done_count"} for o in outs])
+    return rows
+
+
+def per_env(rows, group, n_env):
+    seq = {k: [[] for _ in range(n_env)] for k in ("next_state", "reward", "done", "status", "action")}
+    for launch in rows:
+        o = launch[group]
+        st = o["status"].astype(np.int64) & 0xFFFFFFFF
+        for k in range(st.shape[0]):
+            for e in np.nonzero((st[k] & _lib.ST_NO_STEP) == 0)[0]:
+                seq["next_state"][e].append(o["next_state"][k, e])
+                seq["reward"][e].append(o["reward"][k, e])
+                seq["done"][e].append(bool(o["done"][k, e]))
+                seq["status"][e].append(int(st[k, e]))
+                seq["action"][e].append(o["action"][k, e])
+    return seq
+
+
+def compare(seq, ref, n_env, n_steps):
+    for e in range(n_env):
+        assert len(seq["reward"][e]) >= n_steps, f"env {e}: only {len(seq['reward'][e])} steps executed"
+        ns = np.array(seq["next_state"][e][:n_steps])
+        err = np.abs(ns - ref["next_state"][:, e]) / np.maximum(np.abs(ref["next_state"][:, e]), OBS_SCALE)
+        assert err.max() <= 1e-9, f"env {e}: next_state rel err {err.max():.3e}"
+        rw = np.array(seq["reward"][e][:n_steps])
+        assert np.abs(rw - ref["reward"][:, e]).max() <= 1e-9 * max(1.0, np.abs(ref["reward"][:, e]).max())
+        assert np.array_equal(np.array(seq["done"][e][:n_steps]), ref["done"][:, e]), f"env {e}: done"
+        got_st, ref_st = np.array(seq["status"][e][:n_steps]), ref["status"][:, e].astype(np.int64)
+        bad = np.nonzero(got_st != ref_st)[0]
+        assert bad.size == 0, f"env {e}: status at step {bad[:3]}: {got_st[bad[:3]]} vs {ref_st[bad[:3]]}"
+        act = np.array(seq["action"][e][:n_steps])
+        sac = ref["action"][:, e, 3] > 0.5
+        assert np.array_equal(act[:, 3] > 0.5, sac), f"env {e}: sampling events"
+        assert np.allclose(act[sac, :3], ref["action"][sac, e, :3], rtol=1e-10, atol=1e-9), f"env {e}: IW"
+
+
+def oracle_run(sc, pol, n_steps, env_id_offset=0):
+    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+    o.reset()
+    o.init_step()
+    return o.policy_rollout(n_steps, SEED, oracle_policy_fn(pol), env_id_offset=env_id_offset)
+
+
+@pytest.mark.parametrize("capacity", [None, 8])
+def test_f64_policy_mode_matches_synchronous_loop(capacity):
+    n_env, chunk, n_launch = 64, 16, 40
+    sc = make_scenario(n_env, cap=32, seed=11)
+    env = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+    env.reset()
+    env.init_step()
+    pol = make_policy(torch.float64, DEV)
+    sm = PolicySampler(env, pol, chunk=chunk, seed=SEED, request_capacity=capacity)
+    seq = per_env(run_gpu(sm, n_launch), 0, n_env)
+    done_steps = min(len(r) for r in seq["reward"])
+    executed = int(sm.env_steps.item())
+    assert executed == sum(len(r) for r in seq["reward"])
+    assert done_steps >= 200, done_steps
+    ref = oracle_run(sc, make_policy(torch.float64, "cpu"), done_steps)
+    compare(seq, ref, n_env, done_steps)
+    # the actor saw sampling events of every env (init events at least)
+    assert int(sm.served.item()) >= n_env
+
+
+def test_f64_overlapped_groups_match():
+    n_env, chunk, n_launch = 32, 16, 30
+    sc_all = make_scenario(2 * n_env, cap=32, seed=12)
+    groups = []
+    for g in range(2):
+        sl = slice(g * n_env, (g + 1) * n_env)
+        from sac_maritime_ast_amd.scenario import Scenario
+        sc = Scenario(sc_all.routes[sl], sc_all.n_wpt[sl], sc_all.init[sl], sc_all.polys)
+        env = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+        env.reset()
+        env.init_step()
+        groups.append((sc, PolicySampler(env, make_policy(torch.float64, DEV), chunk=chunk, seed=SEED,
+                                         env_id_offset=g * n_env)))
+    ov = OverlappedPolicySampler([s for _, s in groups])
+    rows = run_gpu(ov, n_launch)
+    ref = None
+    for g, (sc, _) in enumerate(groups):
+        seq = per_env(rows, g, n_env)
+        n = min(len(r) for r in seq["reward"])
+        assert n >= 150, n
+        ref = oracle_run(sc, make_policy(torch.float64, "cpu"), n, env_id_offset=g * n_env)
+        compare(seq, ref, n_env, n)
+
+
+def test_f32_policy_mode_sanity():
+    n_env = 4096
+    env = VecMultiShipRLEnv(scenario=make_scenario(n_env, cap=48), precision=32, device=DEV)
+    env.reset()
+    env.init_step()
+    sm = PolicySampler(env, make_policy(torch.float32, DEV), chunk=32, seed=SEED, request_capacity=1024)
+    stepped = 0
+    for _ in range(20):
+        out = sm.launch()
+        st = out["status"].to(torch.int64) & 0xFFFFFFFF
+        live = (st & _lib.ST_NO_STEP) == 0
+        stepped += int(live.sum().item())
+        assert torch.isfinite(out["next_state"][live]).all()
+        assert torch.isfinite(out["reward"][live]).all()
+    assert stepped == int(sm.env_steps.item())
+    assert stepped > 0.8 * 20 * 32 * n_env
