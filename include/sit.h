@@ -302,6 +302,15 @@ typedef struct sit_rollout_args {
 } sit_rollout_args;
 int sit_rollout(sit_handle* h, const sit_rollout_args* a, void* stream);
 size_t sit_rollout_args_size(void);
+/* Policy mode helper: the squashed Gaussian head of the actor (ast_core/distributions/normal.py:
+ * 88-101, ast_core/policies/gaussian_policy.py:71-72) applied to the actor network's output and
+ * scattered into the env action slots, for request rows q < *request_count:
+ *   x = mu + exp(clip(log_sigma, -20, 2)) * noise[q]   (x = mu when deterministic != 0)
+ *   policy_action[request_env[q]] = tanh(x); policy_ready[request_env[q]] = 1
+ * head real[capacity][head_stride] holds (mu, log_sigma) in its first two columns. */
+int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t head_stride,
+                     const void* noise, const int32_t* request_env, const int32_t* request_count,
+                     int32_t deterministic, void* policy_action, int32_t* policy_ready, void* stream);
 
 /* ---- state export / import (device blob) ------------------------------------------ */
 /* The dynamic state of all envs (ship states, controller integrators, route tables,

@@ -100,6 +100,8 @@ SIGNATURES = {
     "sit_load_routes": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "sit_load_initial": (c_int32, [c_void_p, c_void_p]),
     "sit_map_info": (c_int32, [c_void_p, c_void_p, c_int32]),
+    "sit_policy_apply": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
+                                   c_void_p, c_void_p, c_void_p]),
     "sit_probe_map": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sit_restart": (c_int32, [c_void_p, c_void_p]),
     "sit_reset": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -814,6 +814,25 @@ __global__ __launch_bounds__(256) void k_probe_map(const KArgs<T> a, int n, cons
   if (hull) hull[i] = hull_in_terrain(a.c, a.map, pn, pe, d) ? 1 : 0;
 }
 
+// policy head + scatter (sit_policy_apply, one thread per request row): the squashed Gaussian
+// action tanh(mu + exp(clip(log_sigma, -20, 2)) * noise) (normal.py:88-101, gaussian_policy.py:
+// 71-72) of each queued env, written into its action slot and marked ready
+template <typename T>
+__global__ __launch_bounds__(256) void k_policy_apply(int cap, const T* head, int head_stride, const T* noise,
+                                                      const int32_t* req_env, const int32_t* req_count,
+                                                      int deterministic, T* policy_action, int32_t* policy_ready,
+                                                      int n_env) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap || i >= *req_count) return;
+  const int e = req_env[i];
+  if (e < 0 || e >= n_env) return;
+  const T mu = head[(size_t)i * head_stride];
+  const T ls = xclip(head[(size_t)i * head_stride + 1], T(-20), T(2));
+  const T x = deterministic ? mu : mu + exp(ls) * noise[i];
+  policy_action[e] = tanh(x);
+  policy_ready[e] = 1;
+}
+
 // construction-time state (one thread per env)
 template <typename T>
 __global__ __launch_bounds__(256) void k_restart(const KArgs<T> a) {
@@ -1117,6 +1136,26 @@ int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint
     hipLaunchKernelGGL(k_probe_map<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, n,
                        (const float*)pts_ne, (float*)dist, inside, hull);
   }
+  HIP_TRY(h, hipGetLastError());
+  return SIT_OK;
+}
+
+int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t head_stride, const void* noise,
+                     const int32_t* request_env, const int32_t* request_count, int32_t deterministic,
+                     void* policy_action, int32_t* policy_ready, void* stream) {
+  if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
+  if (capacity <= 0 || !head || head_stride < 2 || !request_env || !request_count || !policy_action ||
+      !policy_ready || (!deterministic && !noise))
+    return fail(h, SIT_E_INVALID, "policy_apply: bad arguments");
+  const int blocks = (capacity + 255) / 256;
+  if (h->precision == SIT_F64)
+    hipLaunchKernelGGL(k_policy_apply<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, capacity,
+                       (const double*)head, head_stride, (const double*)noise, request_env, request_count,
+                       deterministic, (double*)policy_action, policy_ready, h->n_env);
+  else
+    hipLaunchKernelGGL(k_policy_apply<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, capacity,
+                       (const float*)head, head_stride, (const float*)noise, request_env, request_count,
+                       deterministic, (float*)policy_action, policy_ready, h->n_env);
   HIP_TRY(h, hipGetLastError());
   return SIT_OK;
 }

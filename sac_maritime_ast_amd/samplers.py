@@ -141,16 +141,31 @@ class PolicySampler:
 
     @torch.no_grad()
     def act(self):
-        """Actor forward on the queued observations; scatter into the per-env action slots."""
-        io, n = self.io, self.env.n_env
-        count = io["request_count"].clamp(max=self._rows.numel())
-        idx = torch.where(self._rows < count, io["request_env"], n).long()
-        obs = io["request_obs"].to(self.actor_dtype)
-        noise = io["request_noise"].to(self.actor_dtype)
-        action, _, _, _ = self.policy(obs, noise, deterministic=self.deterministic)
-        io["policy_action"].index_put_((idx,), action[:, 0].to(io["policy_action"].dtype))
-        io["policy_ready"].index_put_((idx,), self._one)
-        self.served += count.to(torch.int64)
+        """Actor network (PyTorch-ROCm GEMMs) on the queued observations, then the squashed
+        Gaussian head and the scatter into the per-env action slots in one HIP kernel
+        (sit_policy_apply).  Policies without a `.net` (mu, log_sigma) trunk use the generic
+        path: forward() and a device-side scatter."""
+        io, env = self.io, self.env
+        obs = io["request_obs"] if self.actor_dtype == env.dtype else io["request_obs"].to(self.actor_dtype)
+        net = getattr(self.policy, "net", None)
+        if net is not None and getattr(self.policy, "act_dim", 1) == 1:
+            head = net(obs)
+            if head.dtype != env.dtype:
+                head = head.to(env.dtype)
+            head = head.contiguous()
+            with torch.cuda.device(env.device):
+                env._call("sit_policy_apply", int(self._rows.numel()), head.data_ptr(), int(head.shape[1]),
+                          io["request_noise"].data_ptr(), io["request_env"].data_ptr(),
+                          io["request_count"].data_ptr(), int(bool(self.deterministic)),
+                          io["policy_action"].data_ptr(), io["policy_ready"].data_ptr(), env._stream())
+        else:
+            count = io["request_count"].clamp(max=self._rows.numel())
+            idx = torch.where(self._rows < count, io["request_env"], env.n_env).long()
+            action, _, _, _ = self.policy(obs, io["request_noise"].to(self.actor_dtype),
+                                          deterministic=self.deterministic)
+            io["policy_action"].index_put_((idx,), action[:, 0].to(io["policy_action"].dtype))
+            io["policy_ready"].index_put_((idx,), self._one)
+        self.served += io["request_count"].clamp(max=self._rows.numel())
 
 
 class OverlappedPolicySampler:
