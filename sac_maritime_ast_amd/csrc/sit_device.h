@@ -180,8 +180,20 @@ __device__ __forceinline__ double sampler_normal(uint64_t seed, uint64_t env_id,
 // insertion happens at index -1 (controllers.py:298-303) and never moves it.
 // --------------------------------------------------------------------------------------
 //
-// The active leg (waypoints k-1 and k) is cached in registers: the table is read only when k
-// advances or the route is reloaded, and written only by an insertion, so it stays in HBM.
+// The active leg (waypoints k-1 and k) and the next target (k+1) are cached in registers with
+// their geometry, so the waypoint switch of a step is a register select (no branch around a
+// table read in the step's instruction stream); the next target is refilled by fixup() at the
+// end of the step.  The table is written only by an insertion, so it stays in HBM.
+template <typename T>
+__device__ __forceinline__ void leg_geom(T pn, T pe, T cn, T ce, T& alpha, T& sa, T& ca) {
+  const T dx = cn - pn, dy = ce - pe;
+  alpha = xatan2(dy, dx);
+  const T len = xsqrt(dx * dx + dy * dy);
+  sa = T(0);
+  ca = T(1);
+  if (len > T(0)) { sa = dy / len; ca = dx / len; }
+}
+
 template <typename T>
 struct Route {
   T* tn;          // column base: entry i at tn[i * stride]
@@ -194,19 +206,31 @@ struct Route {
   // the leg's path-tangential angle and its sine/cosine (LOS_guidance.py:110-113) depend only
   // on the two waypoints: computed when the leg changes, not every step (same values)
   T alpha, sa, ca;
+  T nn, ne;                 // waypoint k+1 (the target after a switch)
+  T alpha_n, sa_n, ca_n;    // geometry of the leg k -> k+1
+  bool fix;                 // a switch consumed the next target: refill it (fixup)
   __device__ __forceinline__ T n(int i) const { return (i >= nw - 1) ? end_n : tn[i * stride]; }
   __device__ __forceinline__ T e(int i) const { return (i >= nw - 1) ? end_e : te[i * stride]; }
-  __device__ __forceinline__ void leg_geometry() {
-    const T dx = cn - pn, dy = ce - pe;
-    alpha = xatan2(dy, dx);
-    const T len = xsqrt(dx * dx + dy * dy);
-    sa = T(0);
-    ca = T(1);
-    if (len > T(0)) { sa = dy / len; ca = dx / len; }
+  __device__ __forceinline__ void load_next(int k) {
+    nn = n(k + 1); ne = e(k + 1);
+    leg_geom(cn, ce, nn, ne, alpha_n, sa_n, ca_n);
   }
   __device__ __forceinline__ void load_leg(int k) {
     pn = n(k - 1); pe = e(k - 1); cn = n(k); ce = e(k);
-    leg_geometry();
+    leg_geom(pn, pe, cn, ce, alpha, sa, ca);
+    load_next(k);
+    fix = false;
+  }
+  // NavigationSystem.next_wpt's advance (LOS_guidance.py:88-103) as register selects
+  __device__ __forceinline__ void advance(bool sw, int& k) {
+    k += sw ? 1 : 0;
+    pn = sw ? cn : pn; pe = sw ? ce : pe;
+    cn = sw ? nn : cn; ce = sw ? ne : ce;
+    alpha = sw ? alpha_n : alpha; sa = sw ? sa_n : sa; ca = sw ? ca_n : ca;
+    fix = fix || sw;
+  }
+  __device__ __forceinline__ void fixup(int k) {
+    if (fix) { load_next(k); fix = false; }
   }
   // update_route: insert (in_, ie) at index -1 (controllers.py:298-303); false on overflow
   __device__ __forceinline__ bool insert(T in_, T ie, int k, int cap) {
@@ -215,7 +239,13 @@ struct Route {
     tn[i * stride] = in_;
     te[i * stride] = ie;
     nw += 1;
-    if (k == i) { cn = in_; ce = ie; leg_geometry(); }   // the leg pointed at the final waypoint
+    if (k == i) {                         // the leg pointed at the final waypoint
+      cn = in_; ce = ie;
+      leg_geom(pn, pe, cn, ce, alpha, sa, ca);
+      load_next(k);
+    } else if (k + 1 == i) {              // the next target was the final waypoint
+      load_next(k);
+    }
     return true;
   }
 };
@@ -246,12 +276,7 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
     const double dn = (double)rt.cn - (double)s.n;
     const double de = (double)rt.ce - (double)s.e;
     const double d2 = __dadd_rn(__dmul_rn(dn, dn), __dmul_rn(de, de));
-    if (d2 <= c.ra2 && rt.nw > s.k + 1) {
-      s.k += 1;
-      rt.pn = rt.cn; rt.pe = rt.ce;
-      rt.cn = rt.n(s.k); rt.ce = rt.e(s.k);
-      rt.leg_geometry();
-    }
+    rt.advance(d2 <= c.ra2 && rt.nw > s.k + 1, s.k);
   }
   const T pn = rt.pn, pe = rt.pe;
   const T alpha = rt.alpha, sa = rt.sa, ca = rt.ca;
@@ -290,11 +315,10 @@ __device__ __forceinline__ T power_me_kw(const Consts<T>& c, T thr) {
   return load_me * T(0.001);
 }
 
-// update_differentials + integrate_differentials (ship_model.py:624-643, ship_engine.py:355-395)
+// update_differentials + integrate_differentials; sp, cp = sin/cos of the pre-step heading
+// (computed by the caller at the start of the step, off the guidance dependency chain) (ship_model.py:624-643, ship_engine.py:355-395)
 template <typename T>
-__device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T thr, T rudder) {
-  T sp, cp;
-  xsincos(s.psi, &sp, &cp);
+__device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T thr, T rudder, T sp, T cp) {
   const T u = s.u, v = s.v, r = s.r, w = s.w;
   // kinematics: eta_dot = R(psi) nu
   const T d_n = cp * u - sp * v;
@@ -448,10 +472,14 @@ __device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   const uint32_t rec = reinterpret_cast<const uint32_t*>(m.idx)[cell];
   const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (rec & 0xffffu);
   const int ng = (int)(rec >> 16);
-  T best = T(3.0e38);
+  // every list has >= 1 group (4 ids, padded by repetition); the first is unrolled so its loads
+  // issue without a loop branch in front of them
+  uint2 q = grp[0];
+  T best = xmin(xmin(edge_dist2(m.edge[q.x & 0xffffu], e, n), edge_dist2(m.edge[q.x >> 16], e, n)),
+                xmin(edge_dist2(m.edge[q.y & 0xffffu], e, n), edge_dist2(m.edge[q.y >> 16], e, n)));
 #pragma unroll 1
-  for (int g = 0; g < ng; ++g) {
-    const uint2 q = grp[g];
+  for (int g = 1; g < ng; ++g) {
+    q = grp[g];
     const T d0 = edge_dist2(m.edge[q.x & 0xffffu], e, n);
     const T d1 = edge_dist2(m.edge[q.x >> 16], e, n);
     const T d2 = edge_dist2(m.edge[q.y & 0xffffu], e, n);
@@ -551,8 +579,29 @@ __device__ bool pip_point(const Consts<T>& c, const Map<T>& m, T n, T e) {
 // boundary (dobst: the reward's distance), no corner-centre segment meets a boundary, so all
 // corners share the centre's side and one point test decides.
 template <typename T>
+__device__ bool hull_corners(const Consts<T>& c, const Map<T>& m, T n, T e);
+
+template <typename T>
 __device__ bool hull_in_terrain(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst) {
   if (dobst > c.hull_safe) return pip_point(c, m, n, e);
+  return hull_corners(c, m, n, e);
+}
+
+// the same with the centre's class looked up by the caller (independent of the distance, so its
+// LDS read overlaps the distance computation)
+template <typename T>
+__device__ __forceinline__ bool hull_in_terrain_cls(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst,
+                                                    int cls, int cell, uint32_t word) {
+  if (dobst > c.hull_safe) {
+    if (cls < 2) return cls == 1;
+    if (m.use_cells) return pip_cell(m, cell, word, n, e);
+    return pip_indexed(c, m, n, e);
+  }
+  return hull_corners(c, m, n, e);
+}
+
+template <typename T>
+__device__ bool hull_corners(const Consts<T>& c, const Map<T>& m, T n, T e) {
   const T h = c.half_len;
   // near shore: each corner by its fine-grid class; a corner in a mixed cell by the cell's
   // record (or a band scan without records)

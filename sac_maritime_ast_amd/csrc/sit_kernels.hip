@@ -205,9 +205,11 @@ __device__ __forceinline__ void reset_ship(const Scen<T>& sc, int type, int env,
 // one guidance/control/update/integrate cycle without store, time or bias (MSRL_Env.py:190-217)
 template <typename T>
 __device__ __forceinline__ void init_step_ship(const Consts<T>& c, Ship<T>& s, Route<T>& rt, T v_des) {
-  T rudder, thr, ect;
+  T rudder, thr, ect, sp, cp;
+  xsincos(s.psi, &sp, &cp);
   guidance_control(c, s, rt, v_des, rudder, thr, ect);
-  ship_dynamics(c, s, thr, rudder);
+  ship_dynamics(c, s, thr, rudder, sp, cp);
+  rt.fixup(s.k);
 }
 
 // map bounds check of is_pos_outside_horizon / is_route_outside_horizon (MSRL_env_ex.py:460-542)
@@ -327,6 +329,21 @@ __device__ void diag_wave(int type, int lane, bool act, const int* v) {
 __device__ __forceinline__ void store2(float* p, float a, float b) { *reinterpret_cast<float2*>(p) = make_float2(a, b); }
 __device__ __forceinline__ void store2(double* p, double a, double b) { *reinterpret_cast<double2*>(p) = make_double2(a, b); }
 
+// IW = obstacle position + AB_len (cos, sin)(AB_alpha + a): float trig for the float handle
+// (1e-7 relative of AB_len, inside its 1e-5 contract), double for the float64 handle
+__device__ __forceinline__ void iw_point(float n, float e, double ab_len, double ab_alpha, double ang, float& iwn,
+                                         float& iwe) {
+  float sn, cs;
+  sincosf((float)(ab_alpha + ang), &sn, &cs);
+  iwn = n + (float)ab_len * cs;
+  iwe = e + (float)ab_len * sn;
+}
+__device__ __forceinline__ void iw_point(double n, double e, double ab_len, double ab_alpha, double ang, double& iwn,
+                                         double& iwe) {
+  iwn = n + ab_len * cos(ab_alpha + ang);
+  iwe = e + ab_len * sin(ab_alpha + ang);
+}
+
 constexpr int kExplicit = 0, kSynth = 1, kPolicy = 2;
 constexpr uint32_t kSampGeBit = 1u << 28;   // exchange-only: obstacle sampling distance >= AB_len
 
@@ -405,6 +422,17 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     }
   }
   const T maxn = c.max_n;
+  // per-lane output row pointers, advanced by one row block per step: the loop then needs no
+  // output base pointers in SGPRs (they were re-loaded from the kernel arguments every step)
+  const int outs = __builtin_amdgcn_readfirstlane((a.io.next_state ? 1 : 0) | (a.io.reward ? 2 : 0) |
+                                                  (a.io.done ? 4 : 0) | (a.io.status ? 8 : 0) |
+                                                  (a.io.action_out ? 16 : 0));
+  T* p_ns = (outs & 1) ? a.io.next_state + (size_t)env * SIT_OBS_DIM + (type == 0 ? 0 : 6) : nullptr;
+  T* p_rw = (outs & 2) ? a.io.reward + env : nullptr;
+  uint8_t* p_dn = (outs & 4) ? a.io.done + env : nullptr;
+  uint32_t* p_st = (outs & 8) ? a.io.status + env : nullptr;
+  T* p_ao = (outs & 16) ? a.io.action_out + (size_t)env * 4 : nullptr;
+  const size_t row_step = (size_t)n_env;
   __syncthreads();   // map staged
 #ifdef SIT_DIAG_PHASES
   unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -440,6 +468,8 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       }
     }
     const bool live = act && !stalled;
+    T sp = T(0), cp = T(1);
+    if (live) xsincos(s.psi, &sp, &cp);    // heading trig of the step, off the guidance chain
     if (live) {
       ++n_stepped;
       if (type == 1) {
@@ -449,8 +479,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           sac = need;
           if (sac) {                     // the policy's squashed action scales the route angle
             ang = (double)pa * (M_PI / 6.0);
-            iwn = (T)((double)s.n + ab_len * cos(ab_alpha + ang));
-            iwe = (T)((double)s.e + ab_len * sin(ab_alpha + ang));
+            iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
             ++event;
           }
         } else if (MODE == kSynth) {
@@ -459,8 +488,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           if (sac) {
             const double u01 = sampler_uniform(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
             ang = (u01 * 2.0 - 1.0) * (M_PI / 6.0);
-            iwn = (T)((double)s.n + ab_len * cos(ab_alpha + ang));
-            iwe = (T)((double)s.e + ab_len * sin(ab_alpha + ang));
+            iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
             ++event;
           }
         } else {
@@ -484,7 +512,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           o_rpm = s.w * c.rpm_k;
           o_pme = power_me_kw(c, thr);
           s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
-          ship_dynamics(c, s, thr, rudder);
+          ship_dynamics(c, s, thr, rudder, sp, cp);
           if (!init_f) {                 // distance between the last two stored positions
             const T dn = pre_n - ppn, de = pre_e - ppe;
             const T d = xsqrt(dn * dn + de * de);
@@ -505,7 +533,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         o_rpm = s.w * c.rpm_k;
         o_pme = power_me_kw(c, thr);
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
-        ship_dynamics(c, s, thr, rudder);
+        ship_dynamics(c, s, thr, rudder, sp, cp);
         s.ticks += 1;
       }
 
@@ -518,9 +546,12 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       const bool terrain = false;
 #else
       SIT_PH(0);
+      int cell_c;
+      uint32_t word_c;
+      const int cls_c = fine_lookup(c, map, s.n, s.e, cell_c, word_c);
       const T dobst = distance_indexed(c, map, s.n, s.e);
       SIT_PH(1);
-      const bool terrain = hull_in_terrain(c, map, s.n, s.e, dobst);
+      const bool terrain = hull_in_terrain_cls(c, map, s.n, s.e, dobst, cls_c, cell_c, word_c);
       SIT_PH(2);
 #endif
 #ifdef SIT_DIAG_PATHS
@@ -597,8 +628,8 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     // ---------------- env level: shared reward, outputs ----------------
     bool env_done = false;
     if (MODE == kPolicy && act && !live && type == 0) {   // no step taken this row
-      if (a.io.status) a.io.status[row] = SIT_ST_NO_STEP;
-      if (a.io.done) a.io.done[row] = 0;
+      if (outs & 8) *p_st = SIT_ST_NO_STEP;
+      if (outs & 4) *p_dn = 0;
       if (stall_now) {
         const int q = x.slot[lane];
         if (q < a.io.request_capacity)
@@ -617,8 +648,8 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         const T reward = r_nt + r_term + x.r_nto[lane] + x.r_o[lane] + r_snt + rs;
         const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit | kSampGeBit)) | (coll ? SIT_ST_COLLISION : 0u);
 #ifndef SIT_ABLATE_STORES
-        if (a.io.reward) a.io.reward[row] = reward;
-        if (a.io.done) a.io.done[row] = env_done ? 1 : 0;
+        if (outs & 2) *p_rw = reward;
+        if (outs & 4) *p_dn = env_done ? 1 : 0;
 #endif
         const int slot = x.slot[lane];
         if (slot >= 0 && slot < a.io.transition_capacity) {
@@ -630,26 +661,17 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           rec[22] = (horizon_hit || !env_done) ? T(1) : T(0);
         }
 #ifndef SIT_ABLATE_STORES
-        if (a.io.status) a.io.status[row] = status;
+        if (outs & 8) *p_st = status;
 #endif
 #ifndef SIT_ABLATE_STORES
-        if (a.io.next_state) {
-          T* ns = a.io.next_state + row * SIT_OBS_DIM;
-          store2(ns, s.n, s.e); store2(ns + 2, s.psi, o_rpm); store2(ns + 4, o_ect, o_pme);
-        }
+        if (outs & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_rpm); store2(p_ns + 4, o_ect, o_pme); }
 #endif
       } else {
 #ifndef SIT_ABLATE_STORES
-        if (a.io.next_state) {
-          T* ns = a.io.next_state + row * SIT_OBS_DIM;
-          store2(ns + 6, s.n, s.e); store2(ns + 8, s.psi, o_ect);
-        }
+        if (outs & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_ect); }
 #endif
 #ifndef SIT_ABLATE_STORES
-        if (a.io.action_out) {
-          T* ao = a.io.action_out + row * 4;
-          store2(ao, iwn, iwe); store2(ao + 2, (T)ang, sac ? T(1) : T(0));
-        }
+        if (outs & 16) { store2(p_ao, iwn, iwe); store2(p_ao + 2, (T)ang, sac ? T(1) : T(0)); }
 #endif
         const int slot = x.slot[lane];
         if (slot >= 0 && slot < a.io.transition_capacity) {
@@ -680,6 +702,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     SIT_PH(5);
     // ---------------- auto reset: reset() + init_step() (test_beds/main_ast.py:314-329) ----------------
     if (live) {
+      rt.fixup(s.k);
       ep_step += 1;
 #ifdef SIT_ABLATE_RESET
       if (false) {
@@ -695,6 +718,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       }
     }
     SIT_PH(6);
+    p_ns += row_step * SIT_OBS_DIM;
+    p_rw += row_step;
+    p_dn += row_step;
+    p_st += row_step;
+    p_ao += row_step * 4;
   }
 #ifdef SIT_DIAG_PHASES
   if (lane == 0)
