@@ -83,7 +83,24 @@ DEFAULT_PARAMS = dict(
     theta=2.0, sampling_frequency=7, collision_bias=1,
     e_tolerance=1000.0, arrival_radius=200.0, shaft_rpm_max=2000.0, minimum_ship_distance=50.0,
     bias_throttle_scale=0.5, bias_throttle_max=1.1, bias_rudder_degrees=3.0,
+    # specific fuel consumption coefficients (test_policy.py:162-163: Wartsila 6L26 main engine,
+    # Baudouin 6M26.3 diesel generators; ship_engine.py:89-115)
+    fuel_me_a=128.9, fuel_me_b=-168.9, fuel_me_c=246.8,
+    fuel_dg_a=108.7, fuel_dg_b=-289.9, fuel_dg_c=324.9,
 )
+
+# ShipModelAST.store_simulation_data keys, in order (ship_model.py:645-684)
+LOG_KEYS = ("time [s]", "north position [m]", "east position [m]", "yaw angle [deg]", "rudder angle [deg]",
+            "forward speed [m/s]", "sideways speed [m/s]", "yaw rate [deg/sec]", "propeller shaft speed [rpm]",
+            "commanded load fraction me [-]", "commanded load fraction hsg [-]", "power me [kw]",
+            "available power me [kw]", "power electrical [kw]", "available power electrical [kw]", "power [kw]",
+            "propulsion power [kw]", "fuel rate me [kg/s]", "fuel rate hsg [kg/s]", "fuel rate [kg/s]",
+            "fuel consumption me [kg]", "fuel consumption hsg [kg]", "fuel consumption [kg]", "motor torque [Nm]",
+            "thrust force [kN]", "cross track error [m]", "heading error [deg]")
+# per-step terms behind MultiShipRLEnv.reward_results (MSRL_env_ex.py:628-731, 926-964); the
+# reference keeps their per-episode running sums
+REWARD_TERMS = ("test reward_e_ct", "test reward_near_col", "test total_non_terminal", "obs reward_base",
+                "obs reward_e_ct", "obs reward_near_col", "obs total_non_terminal", "shared total_non_terminal")
 
 # initial-value columns (same order as SIT_INIT_* in include/sit.h)
 INIT_FIELDS = ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed",
@@ -367,7 +384,71 @@ class OracleEnvs:
         for name in ENV_INT:
             s[name] = np.zeros(n, dtype=np.int64)
         s["last_obs"] = self.initial_state.T.astype(np.float64).copy()   # sampler's `state`
+        # logging-only machinery state: accumulated fuel (ship_engine.py:283-289) and the last
+        # logged row (store_last_simulation_data repeats it on the obstacle's stop path)
+        for name in ("fuel_me", "fuel_el", "fuel"):
+            s[name] = np.zeros((2, n))
+        s["last_log"] = np.zeros((2, len(LOG_KEYS), n))
         self.s = s
+        self.log = None          # list of per-step rows when logging (start_log)
+
+    # ---------------- trajectory log (ship_model.py:645-700) ----------------
+    def start_log(self):
+        """Record the reference's simulation_results rows ([2, 27] per env and step) and the
+        reward terms from the next step on; fuel accumulates over logged steps."""
+        self.log = {"ship": [], "reward": []}
+
+    def _distribute_load(self, thr):
+        """MachineryMode.distribute_load(load_perc=thr, hotel_load) (ship_engine.py:46-76)."""
+        c = self.c
+        me, el, hotel = c["main_engine_capacity"], c["electrical_capacity"], c["hotel_load"]
+        total = thr * c["avail_prop"]
+        sg = c["shaft_generator_state"]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            if sg == SG_MOTOR:
+                load_me = np.minimum(total, me)
+                load_el = total + hotel - load_me
+                lp_el = load_el / el
+                lp_me = np.zeros_like(total) if me == 0 else load_me / me
+            elif sg == SG_GEN:
+                load_el = np.full_like(total, min(hotel, el))
+                load_me = total + hotel - load_el
+                lp_me = load_me / me
+                lp_el = np.zeros_like(total) if el == 0 else load_el / el
+            else:
+                load_me = total
+                load_el = np.full_like(total, hotel)
+                lp_me = load_me / me
+                lp_el = load_el / el
+        return load_me, load_el, lp_me, lp_el
+
+    def _log_row(self, t, thr, rudder, ect, psi_ref, pre, m):
+        """store_simulation_data(load_perc=thr, rudder, e_ct, e_psi) from the pre-integration
+        state `pre`; accumulates fuel (BaseMachineryModel.fuel_consumption) where m is set."""
+        c, s = self.c, self.s
+        dt = c["integration_step"]
+        load_me, load_el, lp_me, lp_el = self._distribute_load(thr)
+
+        def spec(x, a, b, cc):                                    # spec_fuel_cons (:257-261)
+            return (a * x ** 2 + b * x + cc) / 3.6e9
+        with np.errstate(invalid="ignore"):
+            rate_me = np.where(load_me == 0, 0.0, load_me * spec(lp_me, c["fuel_me_a"], c["fuel_me_b"], c["fuel_me_c"]))
+            rate_el = np.where(lp_el == 0, 0.0, load_el * spec(lp_el, c["fuel_dg_a"], c["fuel_dg_b"], c["fuel_dg_c"]))
+        s["fuel_me"][t] = np.where(m, s["fuel_me"][t] + rate_me * dt, s["fuel_me"][t])
+        s["fuel_el"][t] = np.where(m, s["fuel_el"][t] + rate_el * dt, s["fuel_el"][t])
+        s["fuel"][t] = np.where(m, s["fuel"][t] + (rate_me + rate_el) * dt, s["fuel"][t])
+        w = pre["shaft_speed"]
+        torque = np.minimum(thr * c["avail_me"] / (w + 0.1), c["avail_me"] / 5 * np.pi / 30)   # ship_engine.py:369-376
+        row = np.stack([
+            s["ticks"][t] * dt, pre["north"], pre["east"], pre["yaw"] * 180 / np.pi, rudder * 180 / np.pi,
+            pre["surge"], pre["sway"], pre["yaw_rate"] * 180 / np.pi, w * 30 / np.pi, lp_me, lp_el,
+            load_me / 1000, np.full_like(thr, c["main_engine_capacity"] / 1000), load_el / 1000,
+            np.full_like(thr, c["electrical_capacity"] / 1000), (load_el + load_me) / 1000,
+            (thr * c["avail_prop"]) / 1000, rate_me, rate_el, rate_me + rate_el,
+            s["fuel_me"][t], s["fuel_el"][t], s["fuel"][t], torque,
+            c["thrust_coeff"] * w * np.abs(w) / 1000, ect,
+            np.abs(pre["yaw"] - psi_ref)])                          # get_heading_error: radians (label says deg)
+        return row
 
     def get_state(self):
         out = {k: v.copy() for k, v in self.s.items()}
@@ -377,7 +458,8 @@ class OracleEnvs:
 
     def set_state(self, st):
         for k in self.s:
-            self.s[k] = np.asarray(st[k]).astype(self.s[k].dtype).copy()
+            if k in st:
+                self.s[k] = np.asarray(st[k]).astype(self.s[k].dtype).copy()
         if "wpt_north" in st:
             self.tab_n = np.asarray(st["wpt_north"], dtype=np.float64).copy()
             self.tab_e = np.asarray(st["wpt_east"], dtype=np.float64).copy()
@@ -536,10 +618,12 @@ class OracleEnvs:
         rpm = s["shaft_speed"][t] * 30 / np.pi
         pme = self._power_me_kw(thr)
         s["last_rpm"][t], s["last_e_ct"][t], s["last_power_me"][t] = rpm, ect, pme
+        pre = {k: s[k][t].copy() for k in ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed")}
+        log = self._log_row(t, thr, rudder, ect, tr["heading_ref"], pre, allm)
         d = self._dynamics(t, thr, rudder, allm)
         s["ticks"][t] += 1
         return dict(rudder=rudder, throttle=thr, heading_ref=tr["heading_ref"], e_ct=ect, rpm=rpm,
-                    power_me=pme, **d)
+                    power_me=pme, log=log, **d)
 
     def reset(self, mask=None):
         """MultiShipRLEnv.reset (MSRL_Env.py:147-188): pose/velocity/time/route/LOS state back to
@@ -577,13 +661,17 @@ class OracleEnvs:
         status = np.zeros(n_env, dtype=np.uint32)
 
         # ---- test_step (MSRL_Env.py:219-285) ----
-        rudder, thr, ect0 = self._guidance_control(0, allm)
+        tr0 = {}
+        rudder, thr, ect0 = self._guidance_control(0, allm, tr0)
         if c["collision_bias"]:  # is_collision_imminent on the all-zero next_states: always True (Q1)
             thr = np.clip(thr * c["bias_throttle_scale"], 0.0, c["bias_throttle_max"])
             rudder = np.clip(rudder + c["bias_rudder"], -c["rudder_max"], c["rudder_max"])
         rpm0 = s["shaft_speed"][0] * 30 / np.pi
         pme0 = self._power_me_kw(thr)
         s["last_rpm"][0], s["last_e_ct"][0], s["last_power_me"][0] = rpm0, ect0, pme0
+        if self.log is not None:       # store_simulation_data before update/integrate (:256-260)
+            pre0 = {k: s[k][0].copy() for k in ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed")}
+            log0 = self._log_row(0, thr, rudder, ect0, tr0["heading_ref"], pre0, allm)
         d0 = self._dynamics(0, thr, rudder, allm)
         s["ticks"][0] += 1
         if trace is not None:
@@ -605,7 +693,16 @@ class OracleEnvs:
         status |= np.where(ins & ~fits, np.uint32(ST_ROUTE_OVERFLOW), np.uint32(0))
         s["sampling_dist"] = np.where(ins, 0.0, s["sampling_dist"])
         pre_n, pre_e = s["north"][1].copy(), s["east"][1].copy()
-        rudder1, thr1, ect1 = self._guidance_control(1, run)
+        tr1 = {}
+        rudder1, thr1, ect1 = self._guidance_control(1, run, tr1)
+        if self.log is not None:       # store_simulation_data / store_last_simulation_data (:294, :367)
+            pre1 = {k: s[k][1].copy() for k in ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed")}
+            row1 = self._log_row(1, thr1, rudder1, ect1, tr1["heading_ref"], pre1, run)
+            last = s["last_log"][1].copy()
+            last[0] = s["ticks"][1] * c["integration_step"]
+            log1 = np.where(run[None, :], row1, last)
+            s["last_log"][1] = log1
+            s["last_log"][0] = log0
         rpm1 = s["shaft_speed"][1] * 30 / np.pi
         pme1 = self._power_me_kw(thr1)
         s["last_rpm"][1] = np.where(run, rpm1, s["last_rpm"][1])
@@ -629,6 +726,9 @@ class OracleEnvs:
         ns[:, 6], ns[:, 7], ns[:, 8] = s["north"][1], s["east"][1], s["yaw"][1]
         ns[:, 9] = s["last_e_ct"][1]
         reward, done, st = self._reward(ns, action_ne)
+        if self.log is not None:
+            self.log["ship"].append(np.stack([log0, log1]))          # [2, 27, n_env]
+            self.log["reward"].append(self._terms)                   # [8, n_env]
         status |= st
         s["ep_step"] += 1
         s["last_obs"] = ns.T.copy()
@@ -657,7 +757,8 @@ class OracleEnvs:
         st = np.zeros(self.n_env, dtype=np.uint32)
         margin = c["length_of_ship"] / 2
         # test ship non-terminal (:628-664)
-        r_ntt = np.abs(t_ect) / tol + (1 - distance_to_polygons(self.polys, tn, te) / maxn) / 100
+        d_t = distance_to_polygons(self.polys, tn, te)
+        r_ntt = np.abs(t_ect) / tol + (1 - d_t / maxn) / 100
         # test ship terminal (:734-809): first satisfied predicate wins the reward
         stop = s["stop"][0].astype(bool)
         rt = np.zeros(self.n_env)
@@ -678,9 +779,12 @@ class OracleEnvs:
         s["stop"][0] = stop.astype(np.int64)
         # obstacle ship non-terminal (:666-710), gated on the stop flag before this call
         ostop = s["stop"][1].astype(bool)
+        d_o = distance_to_polygons(self.polys, on, oe)
         r_nto = np.where(ostop, 0.0,
                          0.1 + (-(np.abs(o_ect) / tol)) / 100
-                         + (-(1 - distance_to_polygons(self.polys, on, oe) / maxn)) / 100)
+                         + (-(1 - d_o / maxn)) / 100)
+        terms_obs = (np.where(ostop, 0.0, 0.1), np.where(ostop, 0.0, -(np.abs(o_ect) / tol) / 100),
+                     np.where(ostop, 0.0, -(1 - d_o / maxn) / 100), r_nto)
         # obstacle ship terminal (:811-881)
         ro = np.zeros(self.n_env)
         done_o = np.zeros(self.n_env, bool)
@@ -709,6 +813,7 @@ class OracleEnvs:
         # shared non-terminal (:712-731): uses the stop flag as just updated
         dist = np.sqrt((tn - on) ** 2 + (te - oe) ** 2)
         r_snt = np.where(ostop, 0.0, (1 - dist / maxn) / 1000)
+        self._terms = np.stack([np.abs(t_ect) / tol, (1 - d_t / maxn) / 100, r_ntt, *terms_obs, r_snt])
         # shared terminal (:883-904)
         coll = (tn - on) ** 2 + (te - oe) ** 2 < c["minimum_ship_distance"] ** 2
         rs = np.where(coll, 2000.0, 0.0)

@@ -248,6 +248,25 @@ def sim_step(ship, thr, ap, bias=False):
     return out
 
 
+# ShipModelAST.store_simulation_data keys in order (ship_model.py:645-684): the trajectory log
+LOG_KEYS = ("time [s]", "north position [m]", "east position [m]", "yaw angle [deg]", "rudder angle [deg]",
+            "forward speed [m/s]", "sideways speed [m/s]", "yaw rate [deg/sec]", "propeller shaft speed [rpm]",
+            "commanded load fraction me [-]", "commanded load fraction hsg [-]", "power me [kw]",
+            "available power me [kw]", "power electrical [kw]", "available power electrical [kw]", "power [kw]",
+            "propulsion power [kw]", "fuel rate me [kg/s]", "fuel rate hsg [kg/s]", "fuel rate [kg/s]",
+            "fuel consumption me [kg]", "fuel consumption hsg [kg]", "fuel consumption [kg]", "motor torque [Nm]",
+            "thrust force [kN]", "cross track error [m]", "heading error [deg]")
+# MultiShipRLEnv.reward_results cumulative series (MSRL_env_ex.py:926-964)
+REWARD_KEYS = (("test_ship", "reward_e_ct"), ("test_ship", "reward_near_col"), ("test_ship", "total_non_terminal"),
+               ("obs_ship", "reward_base"), ("obs_ship", "reward_e_ct"), ("obs_ship", "reward_near_col"),
+               ("obs_ship", "total_non_terminal"), ("shared", "total_non_terminal"))
+
+
+def log_row(ship):
+    res = ship.simulation_results
+    return [float(res[k][-1]) for k in LOG_KEYS]
+
+
 SIM_FIELDS = ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed", "ship_speed_i",
               "shaft_speed_i", "heading_i", "heading_prev", "e_ct_int", "next_wpt")
 OUT_FIELDS = ("rudder", "throttle", "heading_ref", "e_ct", "rpm", "power_me", "d_north", "d_east", "d_yaw",
@@ -271,6 +290,7 @@ def gen_sim_trajectory(ref, name, route, pose, n_steps, bias=False, mode="PTI"):
         o = sim_step(ship, thr, ap, bias)
         for k in OUT_FIELDS:
             out[k].append(o[k])
+        out.setdefault("log", []).append(log_row(ship))
     snap = ship_snapshot(ship, thr, ap)
     r, nr = _route_arrays(route)
     sg, me_cap, el_cap = MODES[mode]
@@ -280,6 +300,7 @@ def gen_sim_trajectory(ref, name, route, pose, n_steps, bias=False, mode="PTI"):
         data["pre_" + k] = np.asarray(pre[k] + [snap[k]], dtype=np.float64)
     for k in OUT_FIELDS:
         data["out_" + k] = np.asarray(out[k], dtype=np.float64)
+    data["log"] = np.asarray(out["log"], dtype=np.float64)      # [n_steps, len(LOG_KEYS)]
     np.savez_compressed(os.path.join(HERE, f"sim_{name}.npz"), **data)
     return data
 
@@ -456,7 +477,9 @@ def run_env_case(ref, obstacle, env_mod, name, n_steps, rng, pose_test=None, pos
         post = env_snapshot(env, iw)
         row = {"action_n": iw[0], "action_e": iw[1], "sac_update": float(sac), "init": float(init),
                "next_state": np.asarray(ns, float), "reward": float(rew), "done": float(done),
-               "status": status}
+               "status": status, "log_test": np.asarray(log_row(env.test.ship_model)),
+               "log_obs": np.asarray(log_row(env.obs.ship_model)),
+               "log_reward": np.asarray([env.reward_results[a][b][-1] for a, b in REWARD_KEYS], float)}
         for k, v in pre.items():
             row["pre_" + k] = np.asarray(v, float)
         for k, v in post.items():

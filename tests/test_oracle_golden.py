@@ -141,3 +141,45 @@ def test_nominal_episode_matches_survey_k4():
     assert len(d["reward"]) == 1694
     assert "Obstacle ship IW sampled in terminal state" in str(d["status"][-1])
     assert d["reward"][-1] == pytest.approx(-999.893291, abs=1e-6)
+
+
+# ------------------------------------------------------------------------------------------
+# trajectory logs: simulation_results (ship_model.py:645-700, fuel model ship_engine.py:256-292)
+# and reward_results (MSRL_env_ex.py:926-964), recorded from the reference by make_golden.py
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", [n for n in golden_names("sim_") if n != "sim_teacher_forced"])
+def test_oracle_simulation_log_vs_reference(name):
+    d = golden(name)
+    o = sim_oracle(d)
+    rows = [o.sim_step(1, bias=bool(d["bias"]))["log"][:, 0] for _ in range(len(d["log"]))]
+    err = np.abs(np.array(rows) - d["log"]) / np.maximum(np.abs(d["log"]), 1.0)
+    assert err.max() <= 1e-10, f"{name}: log rel err {err.max():.3e}"
+
+
+@pytest.mark.parametrize("name", golden_names("env_"))
+def test_oracle_env_logs_vs_reference(name):
+    """Teacher-forced env steps: both ships' simulation_results rows (incl. the obstacle's
+    store_last_simulation_data on the stop path) and the per-episode reward_results sums."""
+    d = golden(name)
+    o = env_oracle(d)
+    o.reset()
+    o.init_step()
+    o.start_log()
+    n = len(d["reward"])
+    for i in range(n):
+        o.set_state(env_state_from(d, "pre_", i, o))
+        o.step(np.array([[d["action_n"][i], d["action_e"][i]]]), [d["sac_update"][i] > 0.5], [d["init"][i] > 0.5])
+    logs = np.array(o.log["ship"])[:, :, :, 0]
+    for t, key in ((0, "log_test"), (1, "log_obs")):
+        err = np.abs(logs[:, t] - d[key]) / np.maximum(np.abs(d[key]), 1.0)
+        assert err.max() <= 1e-10, f"{name} {key}: rel err {err.max():.3e}"
+    terms = np.array(o.log["reward"])[:, :, 0]
+    resets = set(d["resets"].tolist())
+    acc, cum = np.zeros(len(so.REWARD_TERMS)), []
+    for i in range(n):
+        if i in resets:
+            acc = np.zeros(len(so.REWARD_TERMS))
+        acc = acc + terms[i]
+        cum.append(acc.copy())
+    err = np.abs(np.array(cum) - d["log_reward"]) / np.maximum(np.abs(d["log_reward"]), 1.0)
+    assert err.max() <= 1e-12, f"{name} reward_results: rel err {err.max():.3e}"
