@@ -88,6 +88,19 @@ extern "C" {
  *   [10] action (scoping angle a), [11] reward, [12:22] next_state,
  *   [22] mask (1 if the episode step reaches mask_horizon, else not done), [23] env id */
 #define SIT_TRANSITION_DIM 24
+/* Trajectory log rows per env and step (sit_rollout_args.log): ShipModelAST.store_simulation_data's
+ * 27 keys (ship_model.py:645-684, in that order: time [s], north/east position [m], yaw angle
+ * [deg], rudder angle [deg], forward/sideways speed [m/s], yaw rate [deg/sec], propeller shaft
+ * speed [rpm], commanded load fraction me/hsg [-], power me [kw], available power me [kw], power
+ * electrical [kw], available power electrical [kw], power [kw], propulsion power [kw], fuel
+ * rate me/hsg/total [kg/s], fuel consumption me/hsg/total [kg], motor torque [Nm], thrust force
+ * [kN], cross track error [m], heading error [deg] (radians, as the reference stores it)) for
+ * the ship under test (rows 0-26) and the obstacle ship (rows 27-53), then the 8 per-step terms
+ * whose per-episode sums are MultiShipRLEnv.reward_results (MSRL_env_ex.py:926-964): test
+ * reward_e_ct, reward_near_col, total_non_terminal; obstacle reward_base, reward_e_ct,
+ * reward_near_col, total_non_terminal; shared total_non_terminal (rows 54-61). */
+#define SIT_LOG_KEYS 27
+#define SIT_LOG_ROWS 62
 
 /* ---- per-ship initial values for sit_load_initial ---------------------------------- */
 enum {
@@ -179,6 +192,11 @@ typedef struct sit_params {
   double bias_throttle_scale;    /* 0.5  (MSRL_Env.py:246)                     */
   double bias_throttle_max;      /* 1.1  (MSRL_Env.py:247)                     */
   double bias_rudder_degrees;    /* 3    (MSRL_Env.py:250)                     */
+  /* specific fuel consumption a x^2 + b x + c [g/kWh] of the main engine and the diesel
+   * generators (MachinerySystemConfiguration, ship_engine.py:137-138, 89-115; test_policy.py:
+   * 162-163): logging only (trajectory log, fuel keys) */
+  double fuel_me_a, fuel_me_b, fuel_me_c;
+  double fuel_dg_a, fuel_dg_b, fuel_dg_c;
 } sit_params;
 
 /* Fill `p` with the configuration of test_beds/test_policy.py:94-226 (PTI mode). */
@@ -299,6 +317,10 @@ typedef struct sit_rollout_args {
   int32_t* request_count;     /* int32[1] */
   int32_t request_capacity;
   int64_t* env_steps;         /* int64[1] or NULL: += env-steps executed (policy mode) */
+  /* Trajectory log (optional): real[n_steps][SIT_LOG_ROWS][n_env].  The obstacle ship's stop
+   * path repeats its last logged row with the time updated (store_last_simulation_data), and
+   * the fuel consumption accumulates over logged steps only (logging-only quantities). */
+  void* log;
 } sit_rollout_args;
 int sit_rollout(sit_handle* h, const sit_rollout_args* a, void* stream);
 size_t sit_rollout_args_size(void);

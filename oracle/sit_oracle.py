@@ -388,7 +388,7 @@ class OracleEnvs:
         # logged row (store_last_simulation_data repeats it on the obstacle's stop path)
         for name in ("fuel_me", "fuel_el", "fuel"):
             s[name] = np.zeros((2, n))
-        s["last_log"] = np.zeros((2, len(LOG_KEYS), n))
+        s["last_log"] = np.zeros((len(LOG_KEYS), n))          # the obstacle ship's last row
         self.s = s
         self.log = None          # list of per-step rows when logging (start_log)
 
@@ -698,11 +698,10 @@ class OracleEnvs:
         if self.log is not None:       # store_simulation_data / store_last_simulation_data (:294, :367)
             pre1 = {k: s[k][1].copy() for k in ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed")}
             row1 = self._log_row(1, thr1, rudder1, ect1, tr1["heading_ref"], pre1, run)
-            last = s["last_log"][1].copy()
+            last = s["last_log"].copy()
             last[0] = s["ticks"][1] * c["integration_step"]
             log1 = np.where(run[None, :], row1, last)
-            s["last_log"][1] = log1
-            s["last_log"][0] = log0
+            s["last_log"] = log1
         rpm1 = s["shaft_speed"][1] * 30 / np.pi
         pme1 = self._power_me_kw(thr1)
         s["last_rpm"][1] = np.where(run, rpm1, s["last_rpm"][1])

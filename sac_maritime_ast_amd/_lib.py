@@ -18,6 +18,7 @@ SIT_SG_MOTOR, SIT_SG_GEN, SIT_SG_OFF = 0, 1, 2
 SIT_DT_REAL, SIT_DT_I32, SIT_DT_U32 = 0, 1, 2
 SIT_OBS_DIM = 10
 SIT_TRANSITION_DIM = 24
+SIT_LOG_KEYS, SIT_LOG_ROWS = 27, 62
 INIT_FIELDS = ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed", "desired_speed",
                "ship_speed_i", "shaft_speed_i")
 
@@ -56,6 +57,8 @@ PARAM_FIELDS = [
     ("theta", _D), ("sampling_frequency", c_int32), ("collision_bias", c_int32),
     ("e_tolerance", _D), ("arrival_radius", _D), ("shaft_rpm_max", _D), ("minimum_ship_distance", _D),
     ("bias_throttle_scale", _D), ("bias_throttle_max", _D), ("bias_rudder_degrees", _D),
+    ("fuel_me_a", _D), ("fuel_me_b", _D), ("fuel_me_c", _D), ("fuel_dg_a", _D), ("fuel_dg_b", _D),
+    ("fuel_dg_c", _D),
 ]
 
 
@@ -77,7 +80,7 @@ class RolloutArgs(ctypes.Structure):
         ("policy_action", c_void_p), ("policy_ready", c_void_p), ("request_env", c_void_p),
         ("request_noise", c_void_p), ("request_obs", c_void_p), ("request_count", c_void_p),
         ("request_capacity", c_int32),
-        ("env_steps", c_void_p),
+        ("env_steps", c_void_p), ("log", c_void_p),
     ]
 
 

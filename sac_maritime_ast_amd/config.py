@@ -62,6 +62,13 @@ def params_from_reference(ship_config=None, environment_config=None, simulation_
         p.main_engine_capacity = float(mode.main_engine_capacity)
         p.electrical_capacity = float(mode.electrical_capacity)
         p.shaft_generator_state = _SG.get(str(mode.shaft_generator_state), _lib.SIT_SG_OFF)
+        for tag, f in (("me", "specific_fuel_consumption_coefficients_me"),
+                       ("dg", "specific_fuel_consumption_coefficients_dg")):
+            co = getattr(mc, f, None)
+            if co is not None:
+                setattr(p, f"fuel_{tag}_a", float(co.a))
+                setattr(p, f"fuel_{tag}_b", float(co.b))
+                setattr(p, f"fuel_{tag}_c", float(co.c))
     if throttle_gains is not None:
         for f in ("kp_ship_speed", "ki_ship_speed", "kp_shaft_speed", "ki_shaft_speed"):
             setattr(p, f, float(getattr(throttle_gains, f)))

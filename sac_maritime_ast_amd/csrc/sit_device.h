@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sit.h"
+
 namespace sit {
 
 constexpr int kWave = 64;         // CDNA wavefront
@@ -81,6 +83,8 @@ struct Consts {
   T by0, binv;                // band origin and 1 / band height
   T hull_safe;                // half_len * sqrt(2) + 1 m: beyond it all hull corners share the centre's side
   T fx0, fy0, finvx, finvy;   // fine class grid origin and 1 / cell size
+  // trajectory log only (store_simulation_data, fuel model)
+  T el_cap, fuel_me_a, fuel_me_b, fuel_me_c, fuel_dg_a, fuel_dg_b, fuel_dg_c, rad2deg;
 };
 
 // island map (obstacle.py:92-124): edge i of the closed rings runs from (ax, ay) to (bx, by);
@@ -269,7 +273,7 @@ struct Ship {
 // 180-189; LOS_guidance.py:88-121).  Returns rudder, throttle and |e_ct|.
 template <typename T>
 __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s, Route<T>& rt,
-                                                 T v_des, T& rudder, T& thr, T& ect_abs) {
+                                                 T v_des, T& rudder, T& thr, T& ect_abs, T& psi_ref_out) {
   // next_wpt: acceptance test evaluated in double, without contraction, from the stored
   // values (bit-identical to the float64 reference for identical inputs)
   {
@@ -288,6 +292,7 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
   if (xabs(s.ect_int + q) <= c.windup) s.ect_int += q;
   const T chi = xatan(-q - s.ect_int * c.los_ki);
   const T psi_ref = alpha + chi;
+  psi_ref_out = psi_ref;
   // heading PID, error not wrapped (Q4)
   const T err = psi_ref - s.psi;
   const T derr = (err - s.hp) * c.inv_dt;
@@ -302,6 +307,49 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
   const T e2 = wdes - s.u;
   s.i2 = s.i2 + e2 * c.dt;
   thr = e2 * c.kp2 + s.i2 * c.ki2;
+}
+
+// One row of ShipModelAST.store_simulation_data (ship_model.py:645-684) from the pre-integration
+// state s, written to dst[key * stride] for the SIT_LOG_KEYS keys; the fuel accumulators advance
+// (BaseMachineryModel.fuel_consumption, ship_engine.py:263-289; load split
+// MachineryMode.distribute_load, ship_engine.py:46-76; torque :369-376; thrust :363-366).
+template <typename T>
+__device__ void store_log_row(const Consts<T>& c, T* dst, size_t stride, const Ship<T>& s, T thr, T rudder, T ect,
+                              T psi_ref, T& fuel_me, T& fuel_el, T& fuel) {
+  const T total = thr * c.avail_prop;
+  T load_me, load_el, lp_me, lp_el;
+  if (c.sg_mode == 0) {          // MOTOR
+    load_me = xmin(total, c.me_cap);
+    load_el = total + c.hotel - load_me;
+    lp_el = load_el / c.el_cap;
+    lp_me = (c.me_cap == T(0)) ? T(0) : load_me / c.me_cap;
+  } else if (c.sg_mode == 1) {   // GEN
+    load_el = c.load_el_gen;
+    load_me = total + c.hotel - load_el;
+    lp_me = load_me / c.me_cap;
+    lp_el = (c.el_cap == T(0)) ? T(0) : load_el / c.el_cap;
+  } else {                       // OFF
+    load_me = total;
+    load_el = c.hotel;
+    lp_me = load_me / c.me_cap;
+    lp_el = load_el / c.el_cap;
+  }
+  const T rate_me = (load_me == T(0)) ? T(0)
+                    : load_me * ((c.fuel_me_a * lp_me * lp_me + c.fuel_me_b * lp_me + c.fuel_me_c) / T(3.6e9));
+  const T rate_el = (lp_el == T(0)) ? T(0)
+                    : load_el * ((c.fuel_dg_a * lp_el * lp_el + c.fuel_dg_b * lp_el + c.fuel_dg_c) / T(3.6e9));
+  fuel_me = fuel_me + rate_me * c.dt;
+  fuel_el = fuel_el + rate_el * c.dt;
+  fuel = fuel + (rate_me + rate_el) * c.dt;
+  const T w = s.w;
+  const T v[SIT_LOG_KEYS] = {
+      T(s.ticks) * c.dt, s.n, s.e, s.psi * c.rad2deg, rudder * c.rad2deg, s.u, s.v, s.r * c.rad2deg,
+      w * c.rpm_k, lp_me, lp_el, load_me / T(1000), c.me_cap / T(1000), load_el / T(1000),
+      c.el_cap / T(1000), (load_el + load_me) / T(1000), total / T(1000), rate_me, rate_el, rate_me + rate_el,
+      fuel_me, fuel_el, fuel, xmin(thr * c.avail_me / (w + T(0.1)), c.tqcap_me),
+      c.thrust_k * w * xabs(w) / T(1000), ect, xabs(s.psi - psi_ref)};
+#pragma unroll
+  for (int k = 0; k < SIT_LOG_KEYS; ++k) dst[k * stride] = v[k];
 }
 
 // distribute_load(...).load_on_main_engine / 1000 (ship_engine.py:46-76)

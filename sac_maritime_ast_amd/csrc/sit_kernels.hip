@@ -32,7 +32,7 @@ using namespace sit;
 // ---------------------------------------------------------------------------------------
 namespace {
 
-enum Extent { kShip = 0, kEnv = 1, kTable = 2, kObs = 3 };
+enum Extent { kShip = 0, kEnv = 1, kTable = 2, kObs = 3, kLogRow = 4 };
 struct FieldSpec {
   const char* name;
   int dtype;
@@ -59,11 +59,15 @@ const FieldSpec kFields[] = {
     {"episodes", SIT_DT_U32, kEnv},
     {"wpt_north", SIT_DT_REAL, kTable},   {"wpt_east", SIT_DT_REAL, kTable},
     {"last_obs", SIT_DT_REAL, kObs},
+    // trajectory log only: accumulated fuel per ship, the obstacle ship's last logged row
+    {"fuel_me", SIT_DT_REAL, kShip},      {"fuel_el", SIT_DT_REAL, kShip},
+    {"fuel", SIT_DT_REAL, kShip},         {"last_log", SIT_DT_REAL, kLogRow},
 };
 constexpr int kNumFields = (int)(sizeof(kFields) / sizeof(kFields[0]));
 enum FieldId {
   F_NORTH = 0, F_LAST_PME = 14, F_K = 15, F_NW, F_TICKS, F_STOP,
-  F_SAMP = 19, F_IW_E = 24, F_EP = 25, F_EVENT, F_EPISODES, F_WN, F_WE, F_LAST_OBS
+  F_SAMP = 19, F_IW_E = 24, F_EP = 25, F_EVENT, F_EPISODES, F_WN, F_WE, F_LAST_OBS,
+  F_FUEL_ME, F_FUEL_EL, F_FUEL, F_LAST_LOG
 };
 
 // per-env scenario (constant after sit_load_*), device side
@@ -92,6 +96,8 @@ struct State {
   T* wn;                  // [2][cap][n_env]
   T* we;
   T* last_obs;            // [SIT_OBS_DIM][n_env]: observation before the next step
+  T* fuel[3];             // [2 * n_env] each: fuel me, fuel electrical, fuel total (log only)
+  T* last_log;            // [SIT_LOG_KEYS][n_env]: the obstacle's last logged row (log only)
 };
 
 template <typename T>
@@ -122,6 +128,7 @@ struct StepIO {
   int32_t* request_count;
   int32_t request_capacity;
   unsigned long long* env_steps;
+  T* log;                 // [n_steps][SIT_LOG_ROWS][n_env] or null
 };
 
 template <typename T>
@@ -205,9 +212,9 @@ __device__ __forceinline__ void reset_ship(const Scen<T>& sc, int type, int env,
 // one guidance/control/update/integrate cycle without store, time or bias (MSRL_Env.py:190-217)
 template <typename T>
 __device__ __forceinline__ void init_step_ship(const Consts<T>& c, Ship<T>& s, Route<T>& rt, T v_des) {
-  T rudder, thr, ect, sp, cp;
+  T rudder, thr, ect, sp, cp, psi_ref;
   xsincos(s.psi, &sp, &cp);
-  guidance_control(c, s, rt, v_des, rudder, thr, ect);
+  guidance_control(c, s, rt, v_des, rudder, thr, ect, psi_ref);
   ship_dynamics(c, s, thr, rudder, sp, cp);
   rt.fixup(s.k);
 }
@@ -433,6 +440,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   uint32_t* p_st = (outs & 8) ? a.io.status + env : nullptr;
   T* p_ao = (outs & 16) ? a.io.action_out + (size_t)env * 4 : nullptr;
   const size_t row_step = (size_t)n_env;
+  // trajectory log: this ship's column of the step's [SIT_LOG_ROWS][n_env] block
+  T* p_lg = (a.io.log && act) ? a.io.log + (size_t)type * SIT_LOG_KEYS * n_env + env : nullptr;
+  T f_me = T(0), f_el = T(0), f_tot = T(0);
+  if (p_lg) { f_me = a.st.fuel[0][sid]; f_el = a.st.fuel[1][sid]; f_tot = a.st.fuel[2][sid]; }
   __syncthreads();   // map staged
 #ifdef SIT_DIAG_PHASES
   unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -499,6 +510,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         }
         // obs_step (MSRL_Env.py:287-402)
         if (s.stop) {
+          if (p_lg) {                    // store_last_simulation_data: last row, time updated
+            p_lg[0] = T(s.ticks) * c.dt;
+            for (int kk = 1; kk < SIT_LOG_KEYS; ++kk) p_lg[kk * row_step] = a.st.last_log[kk * row_step + env];
+          }
           s.ticks += 2;                  // stop path: next_time() twice, no integration (Q10)
           o_rpm = s.lrpm; o_ect = s.lect; o_pme = s.lpme;
         } else {
@@ -507,11 +522,15 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
             samp = T(0);
           }
           const T pre_n = s.n, pre_e = s.e;
-          T rudder, thr;
-          guidance_control(c, s, rt, v_des, rudder, thr, o_ect);
+          T rudder, thr, psi_ref;
+          guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref);
           o_rpm = s.w * c.rpm_k;
           o_pme = power_me_kw(c, thr);
           s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
+          if (p_lg) {
+            store_log_row(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
+            for (int kk = 0; kk < SIT_LOG_KEYS; ++kk) a.st.last_log[kk * row_step + env] = p_lg[kk * row_step];
+          }
           ship_dynamics(c, s, thr, rudder, sp, cp);
           if (!init_f) {                 // distance between the last two stored positions
             const T dn = pre_n - ppn, de = pre_e - ppe;
@@ -524,8 +543,8 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         }
       } else {
         // test_step (MSRL_Env.py:219-285)
-        T rudder, thr;
-        guidance_control(c, s, rt, v_des, rudder, thr, o_ect);
+        T rudder, thr, psi_ref;
+        guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref);
         if (c.collision_bias) {          // is_collision_imminent() on all-zero states (Q1)
           thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
           rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
@@ -533,6 +552,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         o_rpm = s.w * c.rpm_k;
         o_pme = power_me_kw(c, thr);
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
+        if (p_lg) store_log_row(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
         ship_dynamics(c, s, thr, rudder, sp, cp);
         s.ticks += 1;
       }
@@ -564,6 +584,12 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       bool done = false;
       if (type == 0) {
         r_nt = xabs(o_ect) * c.inv_e_tol + (T(1) - dobst * c.inv_maxn) * T(0.01);
+        if (p_lg) {                      // reward_results terms of the ship under test (:640-643)
+          T* t = p_lg + (size_t)(2 * SIT_LOG_KEYS) * row_step;                 // rows 54-56
+          t[0] = xabs(o_ect) / c.e_tol;
+          t[row_step] = (T(1) - dobst / c.max_n) / T(100);
+          t[2 * row_step] = r_nt;
+        }
         const bool pred[6] = {arrive, horizon, terrain, xabs(o_rpm) > c.rpm_max, xabs(o_ect) > c.e_tol,
                               o_pme > c.blackout_kw};
         const T rew[6] = {T(0), T(0), T(1000), T(1000), T(1000), T(1000)};
@@ -580,6 +606,13 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       } else {
         if (!stop)
           r_nt = T(0.1) - xabs(o_ect) * c.inv_e_tol * T(0.01) - (T(1) - dobst * c.inv_maxn) * T(0.01);
+        if (p_lg) {                      // reward_results terms of the obstacle ship (:656-669)
+          T* t = p_lg + (size_t)(SIT_LOG_KEYS + 3) * row_step;   // rows 57-60
+          t[0] = stop ? T(0) : T(0.1);
+          t[row_step] = stop ? T(0) : -(xabs(o_ect) / c.e_tol) / T(100);
+          t[2 * row_step] = stop ? T(0) : -(T(1) - dobst / c.max_n) / T(100);
+          t[3 * row_step] = r_nt;
+        }
         if (arrive) { stop = 1; bits |= SIT_ST_OBS_ENDPOINT; }
         if (horizon) { stop = 1; done = true; bits |= SIT_ST_OBS_HORIZON; }
         if (terrain) {                   // done without stop flag (Q12)
@@ -644,6 +677,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       if (coll) s.stop = 1;
       if (type == 0) {
         const T r_snt = (bo & kStopBit) ? T(0) : (T(1) - xsqrt(dn * dn + de * de) * c.inv_maxn) * T(0.001);
+        if (p_lg) p_lg[(size_t)(2 * SIT_LOG_KEYS + 7) * row_step] = r_snt;   // shared term (:714-731)
         const T rs = coll ? T(2000) : T(0);
         const T reward = r_nt + r_term + x.r_nto[lane] + x.r_o[lane] + r_snt + rs;
         const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit | kSampGeBit)) | (coll ? SIT_ST_COLLISION : 0u);
@@ -723,6 +757,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     p_dn += row_step;
     p_st += row_step;
     p_ao += row_step * 4;
+    if (p_lg) p_lg += row_step * SIT_LOG_ROWS;
   }
 #ifdef SIT_DIAG_PHASES
   if (lane == 0)
@@ -731,6 +766,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #endif
 
   // ---------------- write back ----------------
+  if (a.io.log && act) { a.st.fuel[0][sid] = f_me; a.st.fuel[1][sid] = f_el; a.st.fuel[2][sid] = f_tot; }
   if (MODE == kPolicy) {
     if (act && type == 1) a.io.policy_ready[env] = ready ? 1 : 0;
     if (a.io.env_steps && type == 0) {   // env-steps executed: one atomic per wave
@@ -1034,6 +1070,10 @@ Consts<T> make_consts(const sit_handle* h) {
   c.by0 = (T)h->by0; c.binv = (T)h->binv;
   c.hull_safe = (T)(l / 2 * std::sqrt(2.0) + 1.0);
   c.fx0 = (T)h->fx0; c.fy0 = (T)h->fy0; c.finvx = (T)h->finvx; c.finvy = (T)h->finvy;
+  c.el_cap = (T)el;
+  c.fuel_me_a = (T)p.fuel_me_a; c.fuel_me_b = (T)p.fuel_me_b; c.fuel_me_c = (T)p.fuel_me_c;
+  c.fuel_dg_a = (T)p.fuel_dg_a; c.fuel_dg_b = (T)p.fuel_dg_b; c.fuel_dg_c = (T)p.fuel_dg_c;
+  c.rad2deg = (T)(180.0 / M_PI);
   return c;
 }
 
@@ -1053,6 +1093,8 @@ KArgs<T> make_args(const sit_handle* h) {
   a.st.episodes = reinterpret_cast<uint32_t*>(h->blob + h->off[F_EPISODES]);
   a.st.wn = fp(F_WN); a.st.we = fp(F_WE);
   a.st.last_obs = fp(F_LAST_OBS);
+  for (int i = 0; i < 3; ++i) a.st.fuel[i] = fp(F_FUEL_ME + i);
+  a.st.last_log = fp(F_LAST_LOG);
   a.sc.init = reinterpret_cast<const T*>(h->scen + h->scen_init);
   a.sc.end_n = reinterpret_cast<const T*>(h->scen + h->scen_end_n);
   a.sc.end_e = reinterpret_cast<const T*>(h->scen + h->scen_end_e);
@@ -1254,6 +1296,9 @@ void sit_params_default(sit_params* p) {
   p->theta = 2; p->sampling_frequency = 7; p->collision_bias = 1;
   p->e_tolerance = 1000; p->arrival_radius = 200; p->shaft_rpm_max = 2000; p->minimum_ship_distance = 50;
   p->bias_throttle_scale = 0.5; p->bias_throttle_max = 1.1; p->bias_rudder_degrees = 3;
+  // SpecificFuelConsumptionWartila6L26 / Baudouin6M26Dot3 (ship_engine.py:89-115), test_policy.py:162-163
+  p->fuel_me_a = 128.9; p->fuel_me_b = -168.9; p->fuel_me_c = 246.8;
+  p->fuel_dg_a = 108.7; p->fuel_dg_b = -289.9; p->fuel_dg_c = 324.9;
 }
 
 const char* sit_last_error(const sit_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
@@ -1285,7 +1330,8 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
   for (int f = 0; f < kNumFields; ++f) {
     int64_t cnt = kFields[f].extent == kShip ? 2LL * n_env
                  : kFields[f].extent == kEnv ? (int64_t)n_env
-                 : kFields[f].extent == kObs ? (int64_t)SIT_OBS_DIM * n_env : 2LL * wpt_capacity * n_env;
+                 : kFields[f].extent == kObs ? (int64_t)SIT_OBS_DIM * n_env
+                 : kFields[f].extent == kLogRow ? (int64_t)SIT_LOG_KEYS * n_env : 2LL * wpt_capacity * n_env;
     const size_t el = kFields[f].dtype == SIT_DT_REAL ? rs : 4;
     h->off[f] = off;
     h->count[f] = cnt;
@@ -1748,6 +1794,7 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     io->request_obs = (R*)ra->request_obs;
     io->request_count = ra->request_count; io->request_capacity = ra->request_capacity;
     io->env_steps = reinterpret_cast<unsigned long long*>(ra->env_steps);
+    io->log = (R*)ra->log;
   };
   if (h->precision == SIT_F64) {
     StepIO<double> io{};

@@ -94,6 +94,8 @@ class VecMultiShipRLEnv:
     def _field_shape(self, name, count):
         if name == "last_obs":
             return (_lib.SIT_OBS_DIM, self.n_env)
+        if name == "last_log":
+            return (_lib.SIT_LOG_KEYS, self.n_env)
         if count == 2 * self.n_env:
             return (2, self.n_env)
         if count == self.n_env:
@@ -171,7 +173,8 @@ class VecMultiShipRLEnv:
     def rollout(self, n_steps: int, seed: int = 25450, auto_reset: bool = True, env_id_offset: int = 0,
                 actions: dict | None = None, out: dict | None = None, want=("next_state", "reward", "done",
                                                                               "status", "action", "done_count"),
-                transition_capacity: int = 0, mask_horizon: int = 600, policy_io: dict | None = None):
+                transition_capacity: int = 0, mask_horizon: int = 600, policy_io: dict | None = None,
+                log: bool = False):
         """K fused steps (one kernel launch).  actions=None: synthetic AST sampler on device.
         Returns a dict of [K, n_env, ...] tensors (reused from `out` when given).  With
         transition_capacity > 0 the sampling-event replay transitions are appended to
@@ -215,6 +218,11 @@ class VecMultiShipRLEnv:
             ra.transition_count = out["transition_count"].data_ptr()
             ra.transition_capacity = int(transition_capacity)
         ra.mask_horizon = int(mask_horizon)
+        if log:                                  # trajectory log [K, SIT_LOG_ROWS, n_env]
+            lg = out.get("log")
+            if lg is None or tuple(lg.shape) != (K, _lib.SIT_LOG_ROWS, n) or lg.dtype != self.dtype:
+                out["log"] = torch.empty((K, _lib.SIT_LOG_ROWS, n), dtype=self.dtype, device=self.device)
+            ra.log = out["log"].data_ptr()
         if policy_io is not None:
             if actions is not None:
                 raise ValueError("policy mode and explicit actions are exclusive")

@@ -319,3 +319,79 @@ def test_f32_sampler_iw_vs_oracle():
     assert np.abs(a[:, 2] - ang_r).max() <= 1e-6
     err = np.abs(a[:, :2] - act_r) / np.maximum(np.abs(act_r), 1e4)
     assert err.max() <= 1e-5, f"IW rel err {err.max():.3e}"
+
+
+# ------------------------------------------------------------------------------------------
+# trajectory logs (simulation_results rows, fuel model, reward_results terms)
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ENV_CASES)
+def test_f64_trajectory_log_vs_reference(name):
+    """The rollout's log (log=True) of recorded episodes against the reference's own
+    simulation_results of both ships and its reward_results running sums."""
+    from sac_maritime_ast_amd.trajectory import reward_results, simulation_results
+    d = golden(name)
+    T = len(d["reward"])
+    env = fixture_env(d, 1, 64)
+    env.reset()
+    o = env_oracle(d)
+    env.set_state(env_state_from(d, "pre_", 0, o))
+    bounds = sorted({0, T, *[int(r) for r in d["resets"] if 0 < r < T]})
+    logs = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        if a > 0:
+            env.reset()
+            env.init_step()
+        acts = {"action_ne": np.stack([d["action_n"][a:b], d["action_e"][a:b]], 1)[:, None, :],
+                "sac_update": d["sac_update"][a:b, None], "init": d["init"][a:b, None]}
+        logs.append(env.rollout(b - a, actions=acts, auto_reset=False, log=True)["log"].cpu().numpy())
+    log = np.concatenate(logs)
+    for ship, key in ((0, "log_test"), (1, "log_obs")):
+        got = np.stack(list(simulation_results(log, 0, ship).values()), axis=1)
+        err = np.abs(got - d[key]) / np.maximum(np.abs(d[key]), 1.0)
+        assert err.max() <= 1e-9, f"{name} {key}: rel err {err.max():.3e} at {np.unravel_index(err.argmax(), err.shape)}"
+    starts = np.zeros(T, bool)
+    starts[[r for r in d["resets"] if 0 <= r < T]] = True
+    rr = reward_results(log, 0, starts)
+    got = np.stack([rr[a][b] for a, b in (("test_ship", "reward_e_ct"), ("test_ship", "reward_near_col"),
+                                          ("test_ship", "total_non_terminal"), ("obs_ship", "reward_base"),
+                                          ("obs_ship", "reward_e_ct"), ("obs_ship", "reward_near_col"),
+                                          ("obs_ship", "total_non_terminal"), ("shared", "total_non_terminal"))], 1)
+    err = np.abs(got - d["log_reward"]) / np.maximum(np.abs(d["log_reward"]), 1.0)
+    assert err.max() <= 1e-9, f"{name} reward_results: rel err {err.max():.3e}"
+
+
+def test_f64_synthetic_rollout_log_vs_oracle():
+    n_env, steps = 512, 400
+    sc = make_scenario(n_env, cap=32)
+    env = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+    env.reset()
+    env.init_step()
+    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+    o.reset()
+    o.init_step()
+    o.start_log()
+    out = env.rollout(steps, seed=77, log=True)
+    o.rollout(steps, seed=77)
+    log = out["log"].cpu().numpy()
+    ref_ship = np.array(o.log["ship"])                 # [K, 2, 27, n]
+    ref = np.concatenate([ref_ship[:, 0], ref_ship[:, 1], np.array(o.log["reward"])], axis=1)
+    err = np.abs(log - ref) / np.maximum(np.abs(ref), 1.0)
+    assert err.max() <= 1e-9, f"log rel err {err.max():.3e} at {np.unravel_index(err.argmax(), err.shape)}"
+    st = np_state(env)
+    for k in ("fuel_me", "fuel_el", "fuel"):
+        assert rel_err(st[k], o.s[k], 1.0).max() <= 1e-9, k
+
+
+def test_f32_rollout_log_sanity():
+    n_env = 4096
+    env = VecMultiShipRLEnv(scenario=make_scenario(n_env, cap=32), precision=32, device=DEV)
+    env.reset()
+    env.init_step()
+    out = env.rollout(200, seed=3, log=True)
+    log = out["log"]
+    assert torch.isfinite(log).all()
+    # the log's pose is the pre-integration state: row k+1's north equals next_state row k's north
+    # for the ship under test when no reset happened in between
+    ns = out["next_state"]
+    same = ~out["done"][:-1].bool()
+    assert torch.equal(log[1:, 1][same], ns[:-1, :, 0][same])
