@@ -313,9 +313,10 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
 // state s, written to dst[key * stride] for the SIT_LOG_KEYS keys; the fuel accumulators advance
 // (BaseMachineryModel.fuel_consumption, ship_engine.py:263-289; load split
 // MachineryMode.distribute_load, ship_engine.py:46-76; torque :369-376; thrust :363-366).
+// (An out-of-line version made the whole step kernel 2.2x slower: calls give it a stack.)
 template <typename T>
-__device__ void store_log_row(const Consts<T>& c, T* dst, size_t stride, const Ship<T>& s, T thr, T rudder, T ect,
-                              T psi_ref, T& fuel_me, T& fuel_el, T& fuel) {
+__device__ __forceinline__ void store_log_row(const Consts<T>& c, T* dst, size_t stride, const Ship<T>& s, T thr,
+                                              T rudder, T ect, T psi_ref, T& fuel_me, T& fuel_el, T& fuel) {
   const T total = thr * c.avail_prop;
   T load_me, load_el, lp_me, lp_el;
   if (c.sg_mode == 0) {          // MOTOR

@@ -354,7 +354,7 @@ __device__ __forceinline__ void iw_point(double n, double e, double ab_len, doub
 constexpr int kExplicit = 0, kSynth = 1, kPolicy = 2;
 constexpr uint32_t kSampGeBit = 1u << 28;   // exchange-only: obstacle sampling distance >= AB_len
 
-template <typename T, int MODE, bool LDSMAP>
+template <typename T, int MODE, bool LDSMAP, bool LOG>
 __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Xchg<T> xs[2];
@@ -441,7 +441,8 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   T* p_ao = (outs & 16) ? a.io.action_out + (size_t)env * 4 : nullptr;
   const size_t row_step = (size_t)n_env;
   // trajectory log: this ship's column of the step's [SIT_LOG_ROWS][n_env] block
-  T* p_lg = (a.io.log && act) ? a.io.log + (size_t)type * SIT_LOG_KEYS * n_env + env : nullptr;
+  // (LOG is a template parameter so the logging code costs the step loop nothing when off)
+  T* p_lg = (LOG && a.io.log && act) ? a.io.log + (size_t)type * SIT_LOG_KEYS * n_env + env : nullptr;
   T f_me = T(0), f_el = T(0), f_tot = T(0);
   if (p_lg) { f_me = a.st.fuel[0][sid]; f_el = a.st.fuel[1][sid]; f_tot = a.st.fuel[2][sid]; }
   __syncthreads();   // map staged
@@ -766,7 +767,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #endif
 
   // ---------------- write back ----------------
-  if (a.io.log && act) { a.st.fuel[0][sid] = f_me; a.st.fuel[1][sid] = f_el; a.st.fuel[2][sid] = f_tot; }
+  if (LOG && a.io.log && act) { a.st.fuel[0][sid] = f_me; a.st.fuel[1][sid] = f_el; a.st.fuel[2][sid] = f_tot; }
   if (MODE == kPolicy) {
     if (act && type == 1) a.io.policy_ready[env] = ready ? 1 : 0;
     if (a.io.env_steps && type == 0) {   // env-steps executed: one atomic per wave
@@ -948,7 +949,7 @@ struct sit_handle {
   size_t map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0, map_frank = 0, map_crec = 0, map_clive = 0;
   int use_cells = 0;
   int64_t n_mixed = 0, n_live = 0;
-  int lds_attr[6] = {-1, -1, -1, -1, -1, -1};   // dynamic-LDS size set per step-kernel variant
+  int lds_attr[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
@@ -1145,7 +1146,7 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   auto go = [&](auto kern) -> int {
     // the dynamic-LDS attribute is set once per kernel and size (not per launch: launches may be
     // captured into HIP graphs)
-    const int slot = mode * 2 + (lds_map ? 1 : 0);
+    const int slot = (mode * 2 + (lds_map ? 1 : 0)) * 2 + (io.log ? 1 : 0);
     if (lds_map && h->lds_attr[slot] != (int)lds) {
       HIP_TRY(h, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       h->lds_attr[slot] = (int)lds;
@@ -1153,10 +1154,15 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(128), lds, stream, a);
     return SIT_OK;
   };
+  auto pick = [&](auto mode_tag) -> int {
+    constexpr int M = decltype(mode_tag)::value;
+    if (io.log) return lds_map ? go(k_env_steps<T, M, true, true>) : go(k_env_steps<T, M, false, true>);
+    return lds_map ? go(k_env_steps<T, M, true, false>) : go(k_env_steps<T, M, false, false>);
+  };
   int rc;
-  if (mode == kSynth) rc = lds_map ? go(k_env_steps<T, kSynth, true>) : go(k_env_steps<T, kSynth, false>);
-  else if (mode == kPolicy) rc = lds_map ? go(k_env_steps<T, kPolicy, true>) : go(k_env_steps<T, kPolicy, false>);
-  else rc = lds_map ? go(k_env_steps<T, kExplicit, true>) : go(k_env_steps<T, kExplicit, false>);
+  if (mode == kSynth) rc = pick(std::integral_constant<int, kSynth>{});
+  else if (mode == kPolicy) rc = pick(std::integral_constant<int, kPolicy>{});
+  else rc = pick(std::integral_constant<int, kExplicit>{});
   if (rc) return rc;
   HIP_TRY(h, hipGetLastError());
   return SIT_OK;
