@@ -41,7 +41,7 @@ def parse():
                     "starts synchronised; ~40k steps reach the steady state of desynchronised episodes)")
     ap.add_argument("--n-env", type=int, default=32768, help="two-ship envs per GPU (32768 = 64k ships)")
     ap.add_argument("--chunk", type=int, default=None,
-                    help="env steps fused per kernel launch (default 200; 32 in policy mode)")
+                    help="env steps fused per kernel launch (default 1000; 32 in policy mode)")
     ap.add_argument("--precision", type=int, default=32, choices=(32, 64))
     ap.add_argument("--seed", type=int, default=25450)
     ap.add_argument("--mode", default="rollout", choices=("rollout", "step", "policy"),
@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--launch-trace", action="store_true", help="print every launch's kernel ms to stderr")
     args = ap.parse_args()
     if args.chunk is None:
-        args.chunk = 32 if args.mode == "policy" else 200
+        args.chunk = 32 if args.mode == "policy" else 1000
     return args
 
 
@@ -74,15 +74,17 @@ def algorithmic_bytes_per_launch(n_env, k, rs, mean_nw_obs, mean_nw_test, mode):
     return n_env * per_env
 
 
-def latest_pmc(precision, mode):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this config, if any."""
+def latest_pmc(precision, mode, n_env, chunk):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this exact launch
+    configuration (precision, mode, envs, steps per launch), if any."""
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("precision") == precision and d.get("mode") == mode and d.get("n_env") == 32768:
+        if (d.get("precision") == precision and d.get("mode") == mode and d.get("n_env") == n_env
+                and d.get("steps_per_launch") == chunk):
             best = d
     return best
 
@@ -212,7 +214,7 @@ def bench_rollout(args, rank, world, dev):
     alg = algorithmic_bytes_per_launch(n_env, chunk, rs, float(st["n_wpt"][1].double().mean().item()),
                                        float(st["n_wpt"][0].double().mean().item()), args.mode)
     env_steps = world * n_env * steps
-    rl = roofline(alg, kern_ms, latest_pmc(args.precision, args.mode))
+    rl = roofline(alg, kern_ms, latest_pmc(args.precision, args.mode, n_env, chunk))
     rl["algorithmic_bytes_per_env_step"] = alg / (n_env * chunk)
     rl["launch_ms"] = stats_of(launch_ms)
     workload = ("C3: 65 536 ships = 32 768 two-ship envs per GPU, random IW actions, auto-reset" if world == 1 else

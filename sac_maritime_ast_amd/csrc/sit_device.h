@@ -233,6 +233,19 @@ struct Route {
     alpha = sw ? alpha_n : alpha; sa = sw ? sa_n : sa; ca = sw ? ca_n : ca;
     fix = fix || sw;
   }
+  // the cached leg state (k, leg, next target, geometry) of a given route length, for register
+  // copies of an episode start (reset restores the construction route, Q16)
+  struct Leg {
+    T pn, pe, cn, ce, nn, ne, alpha, sa, ca, alpha_n, sa_n, ca_n;
+  };
+  __device__ __forceinline__ Leg leg() const {
+    return Leg{pn, pe, cn, ce, nn, ne, alpha, sa, ca, alpha_n, sa_n, ca_n};
+  }
+  __device__ __forceinline__ void set_leg(const Leg& l) {
+    pn = l.pn; pe = l.pe; cn = l.cn; ce = l.ce; nn = l.nn; ne = l.ne;
+    alpha = l.alpha; sa = l.sa; ca = l.ca; alpha_n = l.alpha_n; sa_n = l.sa_n; ca_n = l.ca_n;
+    fix = false;
+  }
   __device__ __forceinline__ void fixup(int k) {
     if (fix) { load_next(k); fix = false; }
   }

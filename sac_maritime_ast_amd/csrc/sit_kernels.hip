@@ -429,6 +429,21 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     }
   }
   const T maxn = c.max_n;
+  // episode-start values held in registers (auto-reset reloads nothing from memory): the
+  // construction pose, route length, first leg with its geometry, and initial observation
+  T p0[6] = {};
+  T lo0[6] = {};
+  int nw0 = 0;
+  typename Route<T>::Leg leg0{};
+  if (act) {
+    for (int j = 0; j < 6; ++j) p0[j] = init_val(a.sc, type, SIT_INIT_NORTH + j, env, n_env);
+    for (int j = 0; j < lo_n; ++j) lo0[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + lo_base + j];
+    nw0 = a.sc.nw0[sid];
+    Route<T> r0 = rt;
+    r0.nw = nw0;
+    r0.load_leg(1);
+    leg0 = r0.leg();
+  }
   // per-lane output row pointers, advanced by one row block per step: the loop then needs no
   // output base pointers in SGPRs (they were re-loaded from the kernel arguments every step)
   const int outs = __builtin_amdgcn_readfirstlane((a.io.next_state ? 1 : 0) | (a.io.reward ? 2 : 0) |
@@ -744,11 +759,14 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #else
       if (a.io.auto_reset && env_done) {
 #endif
-        reset_ship(a.sc, type, env, n_env, s, rt.nw);
-        rt.load_leg(s.k);
+        // reset() (MSRL_Env.py:147-188) from the register copies
+        s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];
+        s.ect_int = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
+        rt.nw = nw0;
+        rt.set_leg(leg0);
         ep_step = 0;
         if (type == 1) { samp = T(0); eps = T(0); ++episodes; }
-        for (int j = 0; j < lo_n; ++j) lo[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + lo_base + j];
+        for (int j = 0; j < 6; ++j) lo[j] = lo0[j];
         init_step_ship(c, s, rt, v_des);
       }
     }
