@@ -92,15 +92,16 @@ struct Consts {
 // LDS base pointer, immediate field offsets) so the predicates need no per-array registers.
 //
 // Spatial index (built on the host by sit_load_map, exact by construction), one u16 array:
-//   idx[0 .. 2*G*G)          grid cell records, one u32 each: first group (in 4-id groups
+//   idx[0 .. 2*G*G)          grid cell records, one u32 each: first group (in 8-byte groups
 //                            from the start of idx) | group count << 16
 //   idx[kBandBase ..]        NB+1 band starts (absolute positions in idx)
 //   then the band entries (edge ids), then the grid groups (8-byte aligned).
 //  * grid: G x G cells over the map extent plus a margin; cell c lists every edge that can be
-//    the nearest edge of some point within 1 m of the cell (conservative bound with a 1 m
-//    float slack), so the minimum over the list equals the minimum over all edges.  A list is
-//    padded to a multiple of 4 with its first id, so one 8-byte LDS read yields 4 ids whose
-//    edge loads are independent (duplicates do not change a minimum).
+//    the nearest edge of some point within 1 m of the cell (conservative prefilter, then a
+//    Lipschitz-sampled refinement with a 1 m float slack; sit_load_map), so the minimum over the
+//    list equals the minimum over all edges.  A list is padded to a multiple of 5 with its first
+//    id and packed as 5 u8 ids per 8-byte group, so one LDS read yields 5 ids whose edge loads
+//    are independent (duplicates do not change a minimum).
 //  * bands: NB horizontal bands; band b lists every edge whose y-range meets the band (+-1 m).
 //    GEOS's ray-crossing test only looks at edges whose y-range contains the point's y.
 //  * classes (separate u32 array): kFine x kFine cells over the map extent + 100 m, 2 bits per
@@ -534,19 +535,21 @@ __device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   const uint32_t rec = reinterpret_cast<const uint32_t*>(m.idx)[cell];
   const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (rec & 0xffffu);
   const int ng = (int)(rec >> 16);
-  // every list has >= 1 group (4 ids, padded by repetition); the first is unrolled so its loads
-  // issue without a loop branch in front of them
+  // every list has >= 1 group (5 u8 ids in 8 bytes, padded by repetition); the first is unrolled
+  // so its loads issue without a loop branch in front of them
   uint2 q = grp[0];
-  T best = xmin(xmin(edge_dist2(m.edge[q.x & 0xffffu], e, n), edge_dist2(m.edge[q.x >> 16], e, n)),
-                xmin(edge_dist2(m.edge[q.y & 0xffffu], e, n), edge_dist2(m.edge[q.y >> 16], e, n)));
+  T best = xmin(xmin(xmin(edge_dist2(m.edge[q.x & 0xffu], e, n), edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n)),
+                     xmin(edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n), edge_dist2(m.edge[q.x >> 24], e, n))),
+                edge_dist2(m.edge[q.y & 0xffu], e, n));
 #pragma unroll 1
   for (int g = 1; g < ng; ++g) {
     q = grp[g];
-    const T d0 = edge_dist2(m.edge[q.x & 0xffffu], e, n);
-    const T d1 = edge_dist2(m.edge[q.x >> 16], e, n);
-    const T d2 = edge_dist2(m.edge[q.y & 0xffffu], e, n);
-    const T d3 = edge_dist2(m.edge[q.y >> 16], e, n);
-    best = xmin(best, xmin(xmin(d0, d1), xmin(d2, d3)));
+    const T d0 = edge_dist2(m.edge[q.x & 0xffu], e, n);
+    const T d1 = edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n);
+    const T d2 = edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n);
+    const T d3 = edge_dist2(m.edge[q.x >> 24], e, n);
+    const T d4 = edge_dist2(m.edge[q.y & 0xffu], e, n);
+    best = xmin(best, xmin(xmin(xmin(d0, d1), xmin(d2, d3)), d4));
   }
   return xsqrt(best);
 }

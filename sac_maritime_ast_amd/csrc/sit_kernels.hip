@@ -286,7 +286,7 @@ __device__ void diag_lane(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst
   const T fx = (e - c.gx0) * c.ginvx, fy = (n - c.gy0) * c.ginvy;
   if (m.use_index && fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)) {
     const int cell = (int)fy * kGrid + (int)fx;
-    v[0] = (int)(reinterpret_cast<const uint32_t*>(m.idx)[cell] >> 16) * 4;
+    v[0] = (int)(reinterpret_cast<const uint32_t*>(m.idx)[cell] >> 16) * 5;
   }
   if (dobst <= c.hull_safe) {
     v[1] = 1;
@@ -1486,8 +1486,16 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
           if (keep[q]) cand[w++] = cand[q];
         cand.resize(w);
       }
-      for (int e : cand) gentries.push_back((uint16_t)e);
-      while ((gentries.size() - first) % 4) gentries.push_back(gentries[first]);
+      // groups of 5 u8 ids in 8 bytes (padded with the list's first id): every list of the
+      // reference map fits one group (lists of 5 near some vertices would need two groups of 4)
+      while (cand.size() % 5) cand.push_back(cand[0]);
+      for (size_t q = 0; q < cand.size(); q += 5) {
+        gentries.push_back((uint16_t)(cand[q] | (cand[q + 1] << 8)));
+        gentries.push_back((uint16_t)(cand[q + 2] | (cand[q + 3] << 8)));
+        gentries.push_back((uint16_t)cand[q + 4]);
+        gentries.push_back(0);
+      }
+      (void)first;
     }
   gstart[kGrid * kGrid] = (uint32_t)gentries.size();
   const double by0 = h->min_n - 1.0, bh = (ext_y + 2.0) / kBands;

@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 args=()
 for lib in "$@"; do
   n=$(basename $lib .so)
-  args+=("$n" 120 env SIT_LIBRARY=$lib python bench.py --no-cpu-baseline --warmup 40000 --steps 20000 "---")
+  args+=("$n" 120 env SIT_LIBRARY=$lib python bench.py --no-cpu-baseline --warmup 40000 --steps 20000 --chunk 200 "---")
   args+=("${n}_c1000" 120 env SIT_LIBRARY=$lib python bench.py --no-cpu-baseline --warmup 40000 --steps 20000 --chunk 1000 "---")
 done
 tools/gpu_steps.sh "${args[@]}"
