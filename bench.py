@@ -155,7 +155,7 @@ def roofline(alg_bytes, kern_ms, pmc):
 def bench_rollout(args, rank, world, dev):
     """Configs C3/C4: synthetic random-IW sampler on device, fused `chunk`-step launches."""
     from sac_maritime_ast_amd import VecMultiShipRLEnv, make_scenario
-    from sac_maritime_ast_amd.shard import TransitionGather, shard_offset
+    from sac_maritime_ast_amd.shard import AsyncTransitionGather, shard_offset
 
     n_env = args.n_env
     offset = shard_offset(rank, n_env)
@@ -170,8 +170,9 @@ def bench_rollout(args, rank, world, dev):
     # replay transitions of sampling events: written by the kernel with a device-side count and
     # all-gathered over RCCL once per launch (no host synchronisation)
     tcap = max(1024, n_env * chunk // 64)
-    gather = TransitionGather(tcap, 24, env.dtype, dev, world) if (world > 1 and not args.no_gather) else None
+    gather = AsyncTransitionGather(tcap, 24, env.dtype, dev, world) if (world > 1 and not args.no_gather) else None
     out = {}
+    launch_no = [0]
 
     if args.mode == "step":   # one sit_step launch per env step, explicit (precomputed) random IWs
         g = torch.Generator(device=dev).manual_seed(args.seed)
@@ -188,22 +189,36 @@ def bench_rollout(args, rank, world, dev):
             env._call("sit_step", act.data_ptr(), sac.data_ptr(), init.data_ptr(), *[b.data_ptr() for b in bufs],
                       env._stream())
     else:
-        def one():
+        def one(ev_pair=None):
+            if gather:     # this launch's slot of the double-buffered transition gather
+                out["transitions"], out["transition_count"] = gather.buffers(launch_no[0])
+            if ev_pair:
+                ev_pair[0].record(stream)
             env.rollout(chunk, seed=args.seed, env_id_offset=offset, out=out,
                         transition_capacity=tcap if gather else 0)
-            if gather:
-                gather(out["transitions"], out["transition_count"])
+            if ev_pair:
+                ev_pair[1].record(stream)
+            if gather:     # RCCL all-gather beside the next launch
+                gather.start(launch_no[0])
+            launch_no[0] += 1
 
     for _ in range(warm // chunk):
         one()
+    if gather:
+        gather.finish()
     n_launch = steps // chunk
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
 
     def run():
         for i in range(n_launch):
-            ev[i][0].record(stream)
-            one()
-            ev[i][1].record(stream)
+            if args.mode == "step":
+                ev[i][0].record(stream)
+                one()
+                ev[i][1].record(stream)
+            else:
+                one(ev[i])
+        if gather:
+            gather.finish()
     elapsed = timed(dev, world, run)
     launch_ms = [a.elapsed_time(b) for a, b in ev]
     if args.launch_trace:
@@ -223,7 +238,8 @@ def bench_rollout(args, rank, world, dev):
         "value": env_steps / elapsed, "steps": steps, "warmup": warm, "ms_per_step": elapsed * 1e3 / steps,
         "config": {"workload": workload, "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env,
                    "fused_steps_per_launch": chunk, "mode": args.mode, "parallelism": f"env-shard x{world}",
-                   "ship_steps_per_s": 2 * env_steps / elapsed, "rccl_transition_gather": gather is not None},
+                   "ship_steps_per_s": 2 * env_steps / elapsed,
+                   "rccl_transition_gather": ("async, double-buffered, per launch" if gather is not None else None)},
         "roofline": rl,
     }
 

@@ -67,3 +67,40 @@ def test_two_rank_shards_equal_one_big_run(tmp_path):
     path = str(tmp_path / "result.txt")
     mp.spawn(_worker, args=(2, _free_port(), path), nprocs=2, join=True)
     assert open(path).read().startswith("ok")
+
+
+def _async_worker(rank, world, port, result_path):
+    """AsyncTransitionGather: double-buffered all-gathers issued asynchronously per launch."""
+    from sac_maritime_ast_amd.shard import AsyncTransitionGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = AsyncTransitionGather(16, 24, torch.float64, "cpu", world)
+        for i in range(5):
+            rec, cnt = g.buffers(i)
+            n = 3 + i + rank                       # rank- and launch-dependent record counts
+            rec.zero_()
+            rec[:n, 0] = float(i)
+            rec[:n, 23] = float(rank)
+            cnt.fill_(n)
+            g.start(i)
+            if i == 3:
+                got = g.records(i)
+                assert got.shape[0] == sum(3 + i + r for r in range(world))
+                assert torch.all(got[:, 0] == i)
+                for r in range(world):
+                    assert int((got[:, 23] == r).sum()) == 3 + i + r
+        g.finish()
+        assert g.launches == 5
+        if rank == 0:
+            with open(result_path, "w") as f:
+                f.write("ok")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_async_transition_gather_two_ranks(tmp_path):
+    path = str(tmp_path / "result_async.txt")
+    mp.spawn(_async_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    assert open(path).read() == "ok"
