@@ -214,8 +214,17 @@ struct Route {
   T nn, ne;                 // waypoint k+1 (the target after a switch)
   T alpha_n, sa_n, ca_n;    // geometry of the leg k -> k+1
   bool fix;                 // a switch consumed the next target: refill it (fixup)
-  __device__ __forceinline__ T n(int i) const { return (i >= nw - 1) ? end_n : tn[i * stride]; }
-  __device__ __forceinline__ T e(int i) const { return (i >= nw - 1) ? end_e : te[i * stride]; }
+  // waypoint i: the table entry, or the final waypoint for i >= nw - 1.  The table is read
+  // unconditionally at min(i, nw - 1) (inside the column: nw <= capacity), so a leg's loads issue
+  // together instead of behind one branch each (one memory round trip per leg reload)
+  __device__ __forceinline__ T n(int i) const {
+    const T v = tn[(i < nw - 1 ? i : nw - 1) * stride];
+    return (i >= nw - 1) ? end_n : v;
+  }
+  __device__ __forceinline__ T e(int i) const {
+    const T v = te[(i < nw - 1 ? i : nw - 1) * stride];
+    return (i >= nw - 1) ? end_e : v;
+  }
   __device__ __forceinline__ void load_next(int k) {
     nn = n(k + 1); ne = e(k + 1);
     leg_geom(cn, ce, nn, ne, alpha_n, sa_n, ca_n);
