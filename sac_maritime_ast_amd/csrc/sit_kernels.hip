@@ -1,1190 +1,22 @@
-// sit_kernels.hip — MI355X (gfx950) kernels and C ABI of the ship-in-transit env step.
-//
-// Layout in HBM (struct of arrays, one device blob, every field 256-B aligned):
-//   ship fields  [2][n_env]   index = type * n_env + env (type 0 = ship under test, 1 = obstacle)
-//   env fields   [n_env]
-//   route tables [2][cap][n_env]  (north and east; waypoint i of env e's ship t at
-//                                  (t * cap + i) * n_env + e, so a wave reads one waypoint
-//                                  index of 64 envs as one coalesced line set)
-// Thread mapping of the step kernel: a 128-thread block owns 64 envs; wave 0 steps their test
-// ships, wave 1 their obstacle ships (different control flow per wave, none inside a wave).
-// The env-level reward needs both ships: each wave evaluates its own ship's termination
-// predicates, the two waves exchange through LDS (double-buffered slots, one barrier per step)
-// and the test-ship wave assembles reward/done/status in the reference's summation order.
-#include <hip/hip_runtime.h>
+// sit_kernels.hip — C ABI of the ship-in-transit env step (include/sit.h) on MI355X (gfx950).
+// Kernels and host helpers: sit_impl.h.  float32 step kernels: sit_steps_f32.hip.
 
-#include <algorithm>
-#include <cmath>
-#include <cstdarg>
-#include <cstdio>
-#include <cstring>
-#include <string>
-#include <type_traits>
-#include <vector>
+#include "sit_impl.h"
 
-#include "sit.h"
-#include "sit_device.h"
-
-using namespace sit;
-
-// ---------------------------------------------------------------------------------------
-// state blob description
-// ---------------------------------------------------------------------------------------
 namespace {
 
-enum Extent { kShip = 0, kEnv = 1, kTable = 2, kObs = 3, kLogRow = 4 };
-struct FieldSpec {
-  const char* name;
-  int dtype;
-  int extent;
-};
-
-constexpr int kShipReal = 15;
-constexpr int kEnvReal = 6;
-const FieldSpec kFields[] = {
-    {"north", SIT_DT_REAL, kShip},        {"east", SIT_DT_REAL, kShip},
-    {"yaw", SIT_DT_REAL, kShip},          {"surge", SIT_DT_REAL, kShip},
-    {"sway", SIT_DT_REAL, kShip},         {"yaw_rate", SIT_DT_REAL, kShip},
-    {"shaft_speed", SIT_DT_REAL, kShip},  {"ship_speed_i", SIT_DT_REAL, kShip},
-    {"shaft_speed_i", SIT_DT_REAL, kShip}, {"heading_i", SIT_DT_REAL, kShip},
-    {"heading_prev", SIT_DT_REAL, kShip}, {"e_ct_int", SIT_DT_REAL, kShip},
-    {"last_rpm", SIT_DT_REAL, kShip},     {"last_e_ct", SIT_DT_REAL, kShip},
-    {"last_power_me", SIT_DT_REAL, kShip},
-    {"next_wpt", SIT_DT_I32, kShip},      {"n_wpt", SIT_DT_I32, kShip},
-    {"ticks", SIT_DT_I32, kShip},         {"stop", SIT_DT_I32, kShip},
-    {"sampling_dist", SIT_DT_REAL, kEnv}, {"eps_dist", SIT_DT_REAL, kEnv},
-    {"prev_pre_north", SIT_DT_REAL, kEnv}, {"prev_pre_east", SIT_DT_REAL, kEnv},
-    {"iw_north", SIT_DT_REAL, kEnv},      {"iw_east", SIT_DT_REAL, kEnv},
-    {"ep_step", SIT_DT_I32, kEnv},        {"event", SIT_DT_U32, kEnv},
-    {"episodes", SIT_DT_U32, kEnv},
-    {"wpt_north", SIT_DT_REAL, kTable},   {"wpt_east", SIT_DT_REAL, kTable},
-    {"last_obs", SIT_DT_REAL, kObs},
-    // trajectory log only: accumulated fuel per ship, the obstacle ship's last logged row
-    {"fuel_me", SIT_DT_REAL, kShip},      {"fuel_el", SIT_DT_REAL, kShip},
-    {"fuel", SIT_DT_REAL, kShip},         {"last_log", SIT_DT_REAL, kLogRow},
-};
-constexpr int kNumFields = (int)(sizeof(kFields) / sizeof(kFields[0]));
-enum FieldId {
-  F_NORTH = 0, F_LAST_PME = 14, F_K = 15, F_NW, F_TICKS, F_STOP,
-  F_SAMP = 19, F_IW_E = 24, F_EP = 25, F_EVENT, F_EPISODES, F_WN, F_WE, F_LAST_OBS,
-  F_FUEL_ME, F_FUEL_EL, F_FUEL, F_LAST_LOG
-};
-
-// per-env scenario (constant after sit_load_*), device side
-template <typename T>
-struct Scen {
-  const T* init;          // [2][SIT_INIT_NF][n_env]
-  const T* end_n;         // [2][n_env]
-  const T* end_e;
-  const int32_t* nw0;     // [2][n_env]
-  const double* ab_len;   // [n_env]
-  const double* ab_alpha; // [n_env]
-  const T* initial_state; // [n_env][10]
-};
-
-template <typename T>
-struct State {
-  T* ship[kShipReal];     // [2 * n_env]
-  int32_t* k;
-  int32_t* nw;
-  int32_t* ticks;
-  int32_t* stop;
-  T* env[kEnvReal];       // sampling_dist, eps_dist, prev_pre_n, prev_pre_e, iw_n, iw_e
-  int32_t* ep_step;
-  uint32_t* event;
-  uint32_t* episodes;
-  T* wn;                  // [2][cap][n_env]
-  T* we;
-  T* last_obs;            // [SIT_OBS_DIM][n_env]: observation before the next step
-  T* fuel[3];             // [2 * n_env] each: fuel me, fuel electrical, fuel total (log only)
-  T* last_log;            // [SIT_LOG_KEYS][n_env]: the obstacle's last logged row (log only)
-};
-
-template <typename T>
-struct StepIO {
-  int32_t n_steps;
-  int32_t auto_reset;
-  uint64_t seed;
-  int64_t env_id_offset;
-  const T* action_ne;
-  const uint8_t* sac_update;
-  const uint8_t* init;
-  T* next_state;
-  T* reward;
-  uint8_t* done;
-  uint32_t* status;
-  T* action_out;
-  int32_t* done_count;
-  T* transitions;
-  int32_t* transition_count;
-  int32_t transition_capacity;
-  int32_t mask_horizon;
-  // policy mode (kPolicy): per-env action slots and the request queue of waiting envs
-  const T* policy_action;
-  int32_t* policy_ready;
-  int32_t* request_env;
-  T* request_noise;
-  T* request_obs;
-  int32_t* request_count;
-  int32_t request_capacity;
-  unsigned long long* env_steps;
-  T* log;                 // [n_steps][SIT_LOG_ROWS][n_env] or null
-};
-
-template <typename T>
-struct KArgs {
-  Consts<T> c;
-  Map<T> map;       // global copy (base pointer = map.off, size map_bytes)
-  State<T> st;
-  Scen<T> sc;
-  StepIO<T> io;
-  int32_t n_env;
-  int32_t cap;
-  int32_t map_bytes;
-};
-
-// Copy the edge records, the packed index and the class grid (the first map_bytes of the map
-// blob) into LDS at `dst`.
-template <typename T>
-__device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* dst) {
-  const unsigned char* src = reinterpret_cast<const unsigned char*>(a.map.edge);
-  const int n16 = a.map_bytes / 16;
-  for (int i = threadIdx.x; i < n16; i += blockDim.x)
-    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-  Map<T> m = a.map;
-  m.edge = reinterpret_cast<const Edge<T>*>(dst);
-  m.idx = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.idx) - src));
-  m.fine = reinterpret_cast<const uint32_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.fine) - src));
-  m.frank = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.frank) - src));
-  m.crec = reinterpret_cast<const uint2*>(dst + (reinterpret_cast<const unsigned char*>(a.map.crec) - src));
-  m.clive = reinterpret_cast<const uint8_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.clive) - src));
-  return m;
-}
-
+#ifdef SIT_SPLIT_F32
 }  // namespace
-
-// ---------------------------------------------------------------------------------------
-// device helpers on the SoA state
-// ---------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void load_ship(const State<T>& st, int sid, Ship<T>& s) {
-  s.n = st.ship[0][sid]; s.e = st.ship[1][sid]; s.psi = st.ship[2][sid];
-  s.u = st.ship[3][sid]; s.v = st.ship[4][sid]; s.r = st.ship[5][sid]; s.w = st.ship[6][sid];
-  s.i1 = st.ship[7][sid]; s.i2 = st.ship[8][sid]; s.hi = st.ship[9][sid]; s.hp = st.ship[10][sid];
-  s.ect_int = st.ship[11][sid]; s.lrpm = st.ship[12][sid]; s.lect = st.ship[13][sid];
-  s.lpme = st.ship[14][sid];
-  s.k = st.k[sid]; s.ticks = st.ticks[sid]; s.stop = st.stop[sid];
-}
-
-template <typename T>
-__device__ __forceinline__ void store_ship(const State<T>& st, int sid, const Ship<T>& s) {
-  st.ship[0][sid] = s.n; st.ship[1][sid] = s.e; st.ship[2][sid] = s.psi;
-  st.ship[3][sid] = s.u; st.ship[4][sid] = s.v; st.ship[5][sid] = s.r; st.ship[6][sid] = s.w;
-  st.ship[7][sid] = s.i1; st.ship[8][sid] = s.i2; st.ship[9][sid] = s.hi; st.ship[10][sid] = s.hp;
-  st.ship[11][sid] = s.ect_int; st.ship[12][sid] = s.lrpm; st.ship[13][sid] = s.lect;
-  st.ship[14][sid] = s.lpme;
-  st.k[sid] = s.k; st.ticks[sid] = s.ticks; st.stop[sid] = s.stop;
-}
-
-template <typename T>
-__device__ __forceinline__ T init_val(const Scen<T>& sc, int type, int f, int env, int n_env) {
-  return sc.init[(type * SIT_INIT_NF + f) * n_env + env];
-}
-
-// MultiShipRLEnv.reset for one ship (MSRL_Env.py:147-188): pose/velocities/time/route/LOS
-// reset; shaft speed and every PI/PID integrator persist (Q6).
-template <typename T>
-__device__ __forceinline__ void reset_ship(const Scen<T>& sc, int type, int env, int n_env, Ship<T>& s,
-                                           int& nw) {
-  s.n = init_val(sc, type, SIT_INIT_NORTH, env, n_env);
-  s.e = init_val(sc, type, SIT_INIT_EAST, env, n_env);
-  s.psi = init_val(sc, type, SIT_INIT_YAW, env, n_env);
-  s.u = init_val(sc, type, SIT_INIT_SURGE, env, n_env);
-  s.v = init_val(sc, type, SIT_INIT_SWAY, env, n_env);
-  s.r = init_val(sc, type, SIT_INIT_YAW_RATE, env, n_env);
-  s.ect_int = T(0);
-  s.k = 1;
-  s.ticks = 0;
-  s.stop = 0;
-  nw = sc.nw0[type * n_env + env];
-}
-
-// one guidance/control/update/integrate cycle without store, time or bias (MSRL_Env.py:190-217)
-template <typename T>
-__device__ __forceinline__ void init_step_ship(const Consts<T>& c, Ship<T>& s, Route<T>& rt, T v_des) {
-  T rudder, thr, ect, sp, cp, psi_ref;
-  xsincos(s.psi, &sp, &cp);
-  guidance_control(c, s, rt, v_des, rudder, thr, ect, psi_ref);
-  ship_dynamics(c, s, thr, rudder, sp, cp);
-  rt.fixup(s.k);
-}
-
-// map bounds check of is_pos_outside_horizon / is_route_outside_horizon (MSRL_env_ex.py:460-542)
-template <typename T>
-__device__ __forceinline__ bool outside(const Consts<T>& c, T n, T e, T margin) {
-  return n < c.min_n + margin || n > c.max_n - margin || e < c.min_e + margin || e > c.max_e - margin;
-}
-
-constexpr uint32_t kStopBit = 1u << 30;   // exchange-only: stop flag after this ship's checks
-constexpr uint32_t kDoneBit = 1u << 29;   // exchange-only: this ship's done
-
-template <typename T>
-struct Xchg {
-  T n[2][kWave];
-  T e[2][kWave];
-  T r_nto[kWave];
-  T r_o[kWave];
-  uint32_t bits[2][kWave];
-  int32_t slot[kWave];    // transition record of this step (obstacle lane allocates)
-};
-
-// ---------------------------------------------------------------------------------------
-// the env step kernel: K steps of MultiShipRLEnv.step (+ optional auto-reset)
-//   MODE  : kExplicit = caller's action arrays, kSynth = synthetic AST sampler on device,
-//           kPolicy = actions from a policy run between launches (an env that reaches a
-//           sampling event without a fresh action waits for the rest of the launch and queues
-//           a request; the next launch consumes the action the policy wrote for it)
-// ---------------------------------------------------------------------------------------
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
-// Diagnostic builds only (tools/diag_paths.py): [type][0..15] predicate path statistics,
-// [type][16..23] shader-clock cycles per step phase (wave lane 0).
-__device__ unsigned long long g_sit_diag[2][32];
-#endif
-#ifdef SIT_DIAG_PHASES
-// per wave of the last launch: start / end (realtime ticks), shader cycles, HW_ID | XCC_ID << 32
-constexpr int kDiagWaves = 8192;
-__device__ unsigned long long g_sit_wave[kDiagWaves][4];
-#endif
-#ifdef SIT_DIAG_PHASES
-// the fence makes the ship state live in registers at the timer, so arithmetic cannot be
-// sunk across a phase boundary
-template <typename T>
-__device__ __forceinline__ void diag_fence(Ship<T>& s) {
-  asm volatile("" : "+v"(s.n), "+v"(s.e), "+v"(s.psi), "+v"(s.u), "+v"(s.v), "+v"(s.r), "+v"(s.w),
-                    "+v"(s.i1), "+v"(s.i2), "+v"(s.hi), "+v"(s.hp), "+v"(s.ect_int));
-  asm volatile("" : "+v"(s.lrpm), "+v"(s.lect), "+v"(s.lpme), "+v"(s.k), "+v"(s.ticks), "+v"(s.stop));
-}
-#define SIT_PH(k) do { diag_fence(s); __builtin_amdgcn_sched_barrier(0); \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph[k] += t_ - ph_t; ph_t = t_; \
-    __builtin_amdgcn_sched_barrier(0); } while (0)
-#else
-#define SIT_PH(k) do { } while (0)
-#endif
-#ifdef SIT_DIAG_PATHS
-
-template <typename T>
-__device__ int diag_band_len(const Consts<T>& c, const Map<T>& m, T n) {
-  const T fb = (n - c.by0) * c.binv;
-  if (!m.use_index || !(fb >= T(0) && fb < T(kBands))) return 0;
-  const int b = (int)fb;
-  return m.idx[kBandBase + b + 1] - m.idx[kBandBase + b];
-}
-
-template <typename T>
-__device__ void diag_lane(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst, bool iw, T iwn, T iwe,
-                          int* v) {
-  const T fx = (e - c.gx0) * c.ginvx, fy = (n - c.gy0) * c.ginvy;
-  if (m.use_index && fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)) {
-    const int cell = (int)fy * kGrid + (int)fx;
-    v[0] = (int)(reinterpret_cast<const uint32_t*>(m.idx)[cell] >> 16) * 5;
-  }
-  if (dobst <= c.hull_safe) {
-    v[1] = 1;
-    const T h = c.half_len;
-    const int c00 = fine_class(c, m, n - h, e - h), c01 = fine_class(c, m, n - h, e + h);
-    const int c10 = fine_class(c, m, n + h, e - h), c11 = fine_class(c, m, n + h, e + h);
-    if (!(c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1)) {
-      if (c00 >= 2 || c01 >= 2) { v[2] += 1; v[3] += diag_band_len(c, m, n - h); }
-      if (c10 >= 2 || c11 >= 2) { v[2] += 1; v[3] += diag_band_len(c, m, n + h); }
-    }
-  } else if (fine_class(c, m, n, e) >= 2) {
-    v[4] = 1;
-    v[3] += diag_band_len(c, m, n);
-  }
-  if (iw && fine_class(c, m, iwn, iwe) >= 2) { v[5] = 1; v[6] = diag_band_len(c, m, iwn); }
-}
-
-__device__ void diag_wave(int type, int lane, bool act, const int* v) {
-  // lane sums and wave maxima / any-counts (the wave pays the max over its lanes)
-  unsigned long long* g = g_sit_diag[type];
-  int mx[7], any[7];
-  for (int j = 0; j < 7; ++j) {
-    int m = act ? v[j] : 0;
-    for (int off = 32; off >= 1; off >>= 1) m = max(m, __shfl_xor(m, off));
-    mx[j] = m;
-    any[j] = __popcll(__ballot(act && v[j] != 0));
-  }
-  if (act) {
-    for (int j = 0; j < 7; ++j) if (v[j]) atomicAdd(&g[j], (unsigned long long)v[j]);
-  }
-  if (lane == 0) {
-    atomicAdd(&g[7], 1ull);
-    atomicAdd(&g[8], (unsigned long long)mx[0]);            // max distance candidates
-    atomicAdd(&g[9], (unsigned long long)(any[1] > 0));     // waves with a near-shore lane
-    atomicAdd(&g[10], (unsigned long long)(any[2] > 0));    // waves with a pair scan
-    atomicAdd(&g[11], (unsigned long long)mx[3]);           // max hull band trips
-    atomicAdd(&g[12], (unsigned long long)(any[4] > 0));    // waves with a mixed far centre
-    atomicAdd(&g[13], (unsigned long long)(any[5] > 0));    // waves with a mixed IW
-    atomicAdd(&g[14], (unsigned long long)mx[6]);           // max IW band trips
-  }
-}
-#endif
-
-// paired output stores: a state row (SIT_OBS_DIM reals) starts 8-byte (float) / 16-byte
-// (double) aligned, so pairs at even offsets go out as one 2-element store (fewer store
-// instructions per wave; the scattered row stride makes store issue, not bytes, the cost)
-__device__ __forceinline__ void store2(float* p, float a, float b) { *reinterpret_cast<float2*>(p) = make_float2(a, b); }
-__device__ __forceinline__ void store2(double* p, double a, double b) { *reinterpret_cast<double2*>(p) = make_double2(a, b); }
-
-// IW = obstacle position + AB_len (cos, sin)(AB_alpha + a): float trig for the float handle
-// (1e-7 relative of AB_len, inside its 1e-5 contract), double for the float64 handle
-__device__ __forceinline__ void iw_point(float n, float e, double ab_len, double ab_alpha, double ang, float& iwn,
-                                         float& iwe) {
-  float sn, cs;
-  sincosf((float)(ab_alpha + ang), &sn, &cs);
-  iwn = n + (float)ab_len * cs;
-  iwe = e + (float)ab_len * sn;
-}
-__device__ __forceinline__ void iw_point(double n, double e, double ab_len, double ab_alpha, double ang, double& iwn,
-                                         double& iwe) {
-  iwn = n + ab_len * cos(ab_alpha + ang);
-  iwe = e + ab_len * sin(ab_alpha + ang);
-}
-
-constexpr int kExplicit = 0, kSynth = 1, kPolicy = 2;
-constexpr uint32_t kSampGeBit = 1u << 28;   // exchange-only: obstacle sampling distance >= AB_len
-
-template <typename T, int MODE, bool LDSMAP, bool LOG>
-__global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ Xchg<T> xs[2];
-#ifdef SIT_DIAG_PHASES
-  const unsigned long long w_t0 = __builtin_amdgcn_s_memtime();
-  const unsigned long long w_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  // The ~70 per-step constants go kernel arguments -> LDS -> VGPRs: loaded through LDS they
-  // land in vector registers (one wave per SIMD leaves ~512 per lane, AGPRs included), whereas
-  // kernel-argument constants compete for the 102 SGPRs and spill to VGPR lanes (v_readlane
-  // in the loop), and reading the LDS block inside the loop put ~40 dependent LDS reads on
-  // each step's critical path (the register copy measured 12% faster).
-  __shared__ Consts<T> cs;
-  for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
-    reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
-  __syncthreads();
-  const Consts<T> c = cs;
-  // LDS: the map blob (edges, index, classes).  Route tables stay in HBM (Route caches the
-  // active leg); keeping the block under 64 KB of LDS matters: a larger allocation measured
-  // ~1.75x slower at the same occupancy-limited grid.
-  const Map<T> map = LDSMAP ? stage_map(a, smem) : a.map;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int type = threadIdx.x >> 6;             // wave-uniform
-  const int n_env = a.n_env;
-  const int env = blockIdx.x * kEnvsPerBlock + lane;
-  const bool act = lane < kEnvsPerBlock && env < n_env;
-  const int sid = type * n_env + env;
-
-  Ship<T> s{};
-  Route<T> rt{};
-  T v_des = T(0);
-  T samp = T(0), eps = T(0), ppn = T(0), ppe = T(0), iwn = T(0), iwe = T(0);
-  // the IW's terrain test is a pure function of (iwn, iwe), which change only at sampling
-  // events (or with the caller's action): cache it
-  T iw_tn = T(0), iw_te = T(0);
-  bool iw_valid = false, iw_in = false;
-  int ep_step = 0;
-  uint32_t event = 0, episodes = 0;
-  double ab_len = 0.0, ab_alpha = 0.0;
-  T lo[6] = {};                      // this ship's part of the last observation
-  const int lo_base = type == 0 ? 0 : 6, lo_n = type == 0 ? 6 : 4;
-  // policy mode: both lanes of an env track whether its next step is a sampling event
-  bool need = false, ready = false, stalled = false;
-  T pa = T(0);
-  uint32_t n_stepped = 0;
-  if (MODE == kPolicy && act) {
-    const double samp0 = (double)a.st.env[0][env];
-    need = a.st.ep_step[env] == 0 || (samp0 >= a.sc.ab_len[env] && a.st.stop[n_env + env] == 0);
-    ready = a.io.policy_ready[env] != 0;
-    pa = a.io.policy_action[env];
-  }
-  if (act) {
-    for (int j = 0; j < lo_n; ++j) lo[j] = a.st.last_obs[(size_t)(lo_base + j) * n_env + env];
-    ep_step = a.st.ep_step[env];
-    load_ship(a.st, sid, s);
-    rt.nw = a.st.nw[sid];
-    rt.end_n = a.sc.end_n[sid];
-    rt.end_e = a.sc.end_e[sid];
-    v_des = init_val(a.sc, type, SIT_INIT_DESIRED_SPEED, env, n_env);
-    rt.tn = a.st.wn + (size_t)type * a.cap * n_env + env;
-    rt.te = a.st.we + (size_t)type * a.cap * n_env + env;
-    rt.stride = n_env;
-    rt.load_leg(s.k);
-    if (type == 1) {
-      samp = a.st.env[0][env]; eps = a.st.env[1][env];
-      ppn = a.st.env[2][env]; ppe = a.st.env[3][env];
-      iwn = a.st.env[4][env]; iwe = a.st.env[5][env];
-      event = a.st.event[env];
-      episodes = a.st.episodes[env];
-      ab_len = a.sc.ab_len[env];
-      ab_alpha = a.sc.ab_alpha[env];
-    }
-  }
-  const T maxn = c.max_n;
-  // episode-start values held in registers (auto-reset reloads nothing from memory): the
-  // construction pose, route length, first leg with its geometry, and initial observation
-  T p0[6] = {};
-  T lo0[6] = {};
-  int nw0 = 0;
-  typename Route<T>::Leg leg0{};
-  if (act) {
-    for (int j = 0; j < 6; ++j) p0[j] = init_val(a.sc, type, SIT_INIT_NORTH + j, env, n_env);
-    for (int j = 0; j < lo_n; ++j) lo0[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + lo_base + j];
-    nw0 = a.sc.nw0[sid];
-    Route<T> r0 = rt;
-    r0.nw = nw0;
-    r0.load_leg(1);
-    leg0 = r0.leg();
-  }
-  // per-lane output row pointers, advanced by one row block per step: the loop then needs no
-  // output base pointers in SGPRs (they were re-loaded from the kernel arguments every step)
-  const int outs = __builtin_amdgcn_readfirstlane((a.io.next_state ? 1 : 0) | (a.io.reward ? 2 : 0) |
-                                                  (a.io.done ? 4 : 0) | (a.io.status ? 8 : 0) |
-                                                  (a.io.action_out ? 16 : 0));
-  T* p_ns = (outs & 1) ? a.io.next_state + (size_t)env * SIT_OBS_DIM + (type == 0 ? 0 : 6) : nullptr;
-  T* p_rw = (outs & 2) ? a.io.reward + env : nullptr;
-  uint8_t* p_dn = (outs & 4) ? a.io.done + env : nullptr;
-  uint32_t* p_st = (outs & 8) ? a.io.status + env : nullptr;
-  T* p_ao = (outs & 16) ? a.io.action_out + (size_t)env * 4 : nullptr;
-  const size_t row_step = (size_t)n_env;
-  // trajectory log: this ship's column of the step's [SIT_LOG_ROWS][n_env] block
-  // (LOG is a template parameter so the logging code costs the step loop nothing when off)
-  T* p_lg = (LOG && a.io.log && act) ? a.io.log + (size_t)type * SIT_LOG_KEYS * n_env + env : nullptr;
-  T f_me = T(0), f_el = T(0), f_tot = T(0);
-  if (p_lg) { f_me = a.st.fuel[0][sid]; f_el = a.st.fuel[1][sid]; f_tot = a.st.fuel[2][sid]; }
-  __syncthreads();   // map staged
-#ifdef SIT_DIAG_PHASES
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long ph_t = __builtin_amdgcn_s_memtime();
-#endif
-
-  for (int step = 0; step < a.io.n_steps; ++step) {
-    const size_t row = (size_t)step * n_env + env;
-    Xchg<T>& x = xs[step & 1];
-    // ---------------- own ship ----------------
-    T o_rpm = T(0), o_ect = T(0), o_pme = T(0);
-    T r_nt = T(0), r_term = T(0);
-    uint32_t bits = 0;
-#ifdef SIT_DIAG_PATHS
-    int dv[7] = {0, 0, 0, 0, 0, 0, 0};
-#endif
-    bool sac = false, init_f = false;
-    double ang = NAN;
-    bool stall_now = false;
-    if (MODE == kPolicy && act && !stalled && need && !ready) {
-      // sampling event without an action: wait for the policy; the obstacle lane queues the
-      // request with this event's standard-normal draw (reparameterised sample, normal.py:96-101)
-      // and its half of the observation; the test lane adds its half after the exchange
-      stalled = stall_now = true;
-      if (type == 1) {
-        const int q = atomicAdd(a.io.request_count, 1);
-        x.slot[lane] = q;
-        if (q < a.io.request_capacity) {
-          a.io.request_env[q] = env;
-          a.io.request_noise[q] = (T)sampler_normal(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
-          for (int j = 0; j < 4; ++j) a.io.request_obs[(size_t)q * SIT_OBS_DIM + 6 + j] = lo[j];
-        }
-      }
-    }
-    const bool live = act && !stalled;
-    T sp = T(0), cp = T(1);
-    if (live) xsincos(s.psi, &sp, &cp);    // heading trig of the step, off the guidance chain
-    if (live) {
-      ++n_stepped;
-      if (type == 1) {
-        // converted_action / SAC_update / init of this step
-        if (MODE == kPolicy) {
-          init_f = (ep_step == 0);
-          sac = need;
-          if (sac) {                     // the policy's squashed action scales the route angle
-            ang = (double)pa * (M_PI / 6.0);
-            iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
-            ++event;
-          }
-        } else if (MODE == kSynth) {
-          init_f = (ep_step == 0);
-          sac = init_f || ((double)samp >= ab_len && !s.stop);
-          if (sac) {
-            const double u01 = sampler_uniform(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
-            ang = (u01 * 2.0 - 1.0) * (M_PI / 6.0);
-            iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
-            ++event;
-          }
-        } else {
-          init_f = a.io.init[row] != 0;
-          sac = a.io.sac_update[row] != 0;
-          iwn = a.io.action_ne[2 * row];
-          iwe = a.io.action_ne[2 * row + 1];
-        }
-        // obs_step (MSRL_Env.py:287-402)
-        if (s.stop) {
-          if (p_lg) {                    // store_last_simulation_data: last row, time updated
-            p_lg[0] = T(s.ticks) * c.dt;
-            for (int kk = 1; kk < SIT_LOG_KEYS; ++kk) p_lg[kk * row_step] = a.st.last_log[kk * row_step + env];
-          }
-          s.ticks += 2;                  // stop path: next_time() twice, no integration (Q10)
-          o_rpm = s.lrpm; o_ect = s.lect; o_pme = s.lpme;
-        } else {
-          if (sac) {                     // update_route: insert at index -1 (Q16)
-            if (!rt.insert(iwn, iwe, s.k, a.cap)) bits |= SIT_ST_ROUTE_OVERFLOW;
-            samp = T(0);
-          }
-          const T pre_n = s.n, pre_e = s.e;
-          T rudder, thr, psi_ref;
-          guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref);
-          o_rpm = s.w * c.rpm_k;
-          o_pme = power_me_kw(c, thr);
-          s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
-          if (p_lg) {
-            store_log_row(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
-            for (int kk = 0; kk < SIT_LOG_KEYS; ++kk) a.st.last_log[kk * row_step + env] = p_lg[kk * row_step];
-          }
-          ship_dynamics(c, s, thr, rudder, sp, cp);
-          if (!init_f) {                 // distance between the last two stored positions
-            const T dn = pre_n - ppn, de = pre_e - ppe;
-            const T d = xsqrt(dn * dn + de * de);
-            eps = eps + d;
-            samp = samp + d;
-          }
-          ppn = pre_n; ppe = pre_e;
-          s.ticks += 1;
-        }
-      } else {
-        // test_step (MSRL_Env.py:219-285)
-        T rudder, thr, psi_ref;
-        guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref);
-        if (c.collision_bias) {          // is_collision_imminent() on all-zero states (Q1)
-          thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
-          rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
-        }
-        o_rpm = s.w * c.rpm_k;
-        o_pme = power_me_kw(c, thr);
-        s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
-        if (p_lg) store_log_row(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
-        ship_dynamics(c, s, thr, rudder, sp, cp);
-        s.ticks += 1;
-      }
-
-      // ---------------- own termination predicates (MSRL_env_ex.py:628-881) ----------------
-#if defined(SIT_ABLATE_PREDICATES)   // diagnostic builds only (tools/ablate.sh): polygon work removed
-      const T dobst = T(1000);
-      const bool terrain = false;
-#elif defined(SIT_ABLATE_HULL)        // diagnostic: distance kept, hull test removed
-      const T dobst = distance_indexed(c, map, s.n, s.e);
-      const bool terrain = false;
-#else
-      SIT_PH(0);
-      int cell_c;
-      uint32_t word_c;
-      const int cls_c = fine_lookup(c, map, s.n, s.e, cell_c, word_c);
-      const T dobst = distance_indexed(c, map, s.n, s.e);
-      SIT_PH(1);
-      const bool terrain = hull_in_terrain_cls(c, map, s.n, s.e, dobst, cls_c, cell_c, word_c);
-      SIT_PH(2);
-#endif
-#ifdef SIT_DIAG_PATHS
-      diag_lane(c, map, s.n, s.e, dobst, type == 1, iwn, iwe, dv);
-#endif
-      const T dn_end = s.n - rt.end_n, de_end = s.e - rt.end_e;
-      const bool arrive = xsqrt(dn_end * dn_end + de_end * de_end) <= c.arrival_radius;
-      const bool horizon = outside(c, s.n, s.e, c.half_len);
-      int stop = s.stop;
-      bool done = false;
-      if (type == 0) {
-        r_nt = xabs(o_ect) * c.inv_e_tol + (T(1) - dobst * c.inv_maxn) * T(0.01);
-        if (p_lg) {                      // reward_results terms of the ship under test (:640-643)
-          T* t = p_lg + (size_t)(2 * SIT_LOG_KEYS) * row_step;                 // rows 54-56
-          t[0] = xabs(o_ect) / c.e_tol;
-          t[row_step] = (T(1) - dobst / c.max_n) / T(100);
-          t[2 * row_step] = r_nt;
-        }
-        const bool pred[6] = {arrive, horizon, terrain, xabs(o_rpm) > c.rpm_max, xabs(o_ect) > c.e_tol,
-                              o_pme > c.blackout_kw};
-        const T rew[6] = {T(0), T(0), T(1000), T(1000), T(1000), T(1000)};
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          if (pred[i]) {
-            if (!stop) r_term = r_term + rew[i];
-            stop = 1;
-            done = true;
-            bits |= 1u << i;
-          }
-        }
-        if (done) bits |= SIT_ST_TEST_DONE;
-      } else {
-        if (!stop)
-          r_nt = T(0.1) - xabs(o_ect) * c.inv_e_tol * T(0.01) - (T(1) - dobst * c.inv_maxn) * T(0.01);
-        if (p_lg) {                      // reward_results terms of the obstacle ship (:656-669)
-          T* t = p_lg + (size_t)(SIT_LOG_KEYS + 3) * row_step;   // rows 57-60
-          t[0] = stop ? T(0) : T(0.1);
-          t[row_step] = stop ? T(0) : -(xabs(o_ect) / c.e_tol) / T(100);
-          t[2 * row_step] = stop ? T(0) : -(T(1) - dobst / c.max_n) / T(100);
-          t[3 * row_step] = r_nt;
-        }
-        if (arrive) { stop = 1; bits |= SIT_ST_OBS_ENDPOINT; }
-        if (horizon) { stop = 1; done = true; bits |= SIT_ST_OBS_HORIZON; }
-        if (terrain) {                   // done without stop flag (Q12)
-          if (!stop) r_term = r_term - T(1000);
-          done = true;
-          bits |= SIT_ST_OBS_TERRAIN;
-        }
-#if defined(SIT_ABLATE_PREDICATES) || defined(SIT_ABLATE_HULL)
-        if (outside(c, iwn, iwe, T(0))) {
-#else
-        if (!iw_valid || iwn != iw_tn || iwe != iw_te) {
-          iw_in = pip_point(c, map, iwn, iwe);
-          iw_tn = iwn; iw_te = iwe; iw_valid = true;
-        }
-        if (outside(c, iwn, iwe, T(0)) || iw_in) {   // Q11
-#endif
-          if (!stop) r_term = r_term - T(1000);
-          stop = 1; done = true;
-          bits |= SIT_ST_OBS_IW_TERMINAL;
-        }
-        if (xabs(o_ect) > c.e_tol || (double)samp > ab_len * (double)c.theta) {
-          if (!stop) r_term = r_term - T(1000);
-          stop = 1; done = true;
-          bits |= SIT_ST_OBS_NAVIGATION;
-        }
-        if (done) bits |= SIT_ST_OBS_DONE;
-      }
-      s.stop = stop;
-      if (type == 1) {
-        int slot = -1;
-        if (a.io.transitions && sac) slot = atomicAdd(a.io.transition_count, 1);
-        x.slot[lane] = slot;
-      }
-      x.n[type][lane] = s.n;
-      x.e[type][lane] = s.e;
-      x.bits[type][lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u) |
-                           ((MODE == kPolicy && type == 1 && (double)samp >= ab_len) ? kSampGeBit : 0u);
-      if (type == 1) { x.r_nto[lane] = r_nt; x.r_o[lane] = r_term; }
-    }
-    SIT_PH(3);
-    __syncthreads();
-    SIT_PH(4);
-#ifdef SIT_DIAG_PATHS
-    diag_wave(type, lane, act, dv);
-#endif
-    // ---------------- env level: shared reward, outputs ----------------
-    bool env_done = false;
-    if (MODE == kPolicy && act && !live && type == 0) {   // no step taken this row
-      if (outs & 8) *p_st = SIT_ST_NO_STEP;
-      if (outs & 4) *p_dn = 0;
-      if (stall_now) {
-        const int q = x.slot[lane];
-        if (q < a.io.request_capacity)
-          for (int j = 0; j < 6; ++j) a.io.request_obs[(size_t)q * SIT_OBS_DIM + j] = lo[j];
-      }
-    }
-    if (live) {
-      const T dn = x.n[0][lane] - x.n[1][lane], de = x.e[0][lane] - x.e[1][lane];
-      const bool coll = dn * dn + de * de < c.min_dist2;
-      const uint32_t bt = x.bits[0][lane], bo = x.bits[1][lane];
-      env_done = ((bt | bo) & kDoneBit) || coll;
-      if (coll) s.stop = 1;
-      if (type == 0) {
-        const T r_snt = (bo & kStopBit) ? T(0) : (T(1) - xsqrt(dn * dn + de * de) * c.inv_maxn) * T(0.001);
-        if (p_lg) p_lg[(size_t)(2 * SIT_LOG_KEYS + 7) * row_step] = r_snt;   // shared term (:714-731)
-        const T rs = coll ? T(2000) : T(0);
-        const T reward = r_nt + r_term + x.r_nto[lane] + x.r_o[lane] + r_snt + rs;
-        const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit | kSampGeBit)) | (coll ? SIT_ST_COLLISION : 0u);
-#ifndef SIT_ABLATE_STORES
-        if (outs & 2) *p_rw = reward;
-        if (outs & 4) *p_dn = env_done ? 1 : 0;
-#endif
-        const int slot = x.slot[lane];
-        if (slot >= 0 && slot < a.io.transition_capacity) {
-          T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
-          for (int j = 0; j < 6; ++j) rec[j] = lo[j];
-          rec[11] = reward;
-          rec[12] = s.n; rec[13] = s.e; rec[14] = s.psi; rec[15] = o_rpm; rec[16] = o_ect; rec[17] = o_pme;
-          const bool horizon_hit = a.io.mask_horizon > 0 && ep_step + 2 == a.io.mask_horizon;
-          rec[22] = (horizon_hit || !env_done) ? T(1) : T(0);
-        }
-#ifndef SIT_ABLATE_STORES
-        if (outs & 8) *p_st = status;
-#endif
-#ifndef SIT_ABLATE_STORES
-        if (outs & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_rpm); store2(p_ns + 4, o_ect, o_pme); }
-#endif
-      } else {
-#ifndef SIT_ABLATE_STORES
-        if (outs & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_ect); }
-#endif
-#ifndef SIT_ABLATE_STORES
-        if (outs & 16) { store2(p_ao, iwn, iwe); store2(p_ao + 2, (T)ang, sac ? T(1) : T(0)); }
-#endif
-        const int slot = x.slot[lane];
-        if (slot >= 0 && slot < a.io.transition_capacity) {
-          T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
-          for (int j = 0; j < 4; ++j) rec[6 + j] = lo[j];
-          rec[10] = (T)ang;
-          rec[18] = s.n; rec[19] = s.e; rec[20] = s.psi; rec[21] = o_ect;
-          if (MODE == kPolicy) rec[10] = pa;   // the policy's action (memory.push, main_ast.py:395)
-          rec[23] = (T)(a.io.env_id_offset + env);
-        }
-      }
-      // the observation becomes the next step's state
-      if (type == 0) { lo[0] = s.n; lo[1] = s.e; lo[2] = s.psi; lo[3] = o_rpm; lo[4] = o_ect; lo[5] = o_pme; }
-      else { lo[0] = s.n; lo[1] = s.e; lo[2] = s.psi; lo[3] = o_ect; }
-      if (MODE == kPolicy) {
-        if (need) ready = false;       // this step's sampling event consumed the action (both lanes)
-        // the next step is a sampling event at an episode start or once the sampling distance
-        // reaches AB_len while the obstacle ship runs (the obstacle lane's own test, exchanged)
-        const bool obs_stop = (bo & kStopBit) || coll;
-        need = ((bo & kSampGeBit) && !obs_stop) || (a.io.auto_reset && env_done);
-      }
-    }
-    // episode-done count: one ballot + popcount per wave, one atomic per wave
-    if (type == 0 && a.io.done_count) {
-      const unsigned long long m = __ballot(env_done);
-      if (lane == 0 && m) atomicAdd(a.io.done_count + step, (int)__popcll(m));
-    }
-    SIT_PH(5);
-    // ---------------- auto reset: reset() + init_step() (test_beds/main_ast.py:314-329) ----------------
-    if (live) {
-      rt.fixup(s.k);
-      ep_step += 1;
-#ifdef SIT_ABLATE_RESET
-      if (false) {
-#else
-      if (a.io.auto_reset && env_done) {
-#endif
-        // reset() (MSRL_Env.py:147-188) from the register copies
-        s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];
-        s.ect_int = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
-        rt.nw = nw0;
-        rt.set_leg(leg0);
-        ep_step = 0;
-        if (type == 1) { samp = T(0); eps = T(0); ++episodes; }
-        for (int j = 0; j < 6; ++j) lo[j] = lo0[j];
-        init_step_ship(c, s, rt, v_des);
-      }
-    }
-    SIT_PH(6);
-    p_ns += row_step * SIT_OBS_DIM;
-    p_rw += row_step;
-    p_dn += row_step;
-    p_st += row_step;
-    p_ao += row_step * 4;
-    if (p_lg) p_lg += row_step * SIT_LOG_ROWS;
-  }
-#ifdef SIT_DIAG_PHASES
-  if (lane == 0)
-    for (int k = 0; k < 7; ++k) atomicAdd(&g_sit_diag[type][16 + k], ph[k]);
-  const unsigned long long w_loop = ph_t;
-#endif
-
-  // ---------------- write back ----------------
-  if (LOG && a.io.log && act) { a.st.fuel[0][sid] = f_me; a.st.fuel[1][sid] = f_el; a.st.fuel[2][sid] = f_tot; }
-  if (MODE == kPolicy) {
-    if (act && type == 1) a.io.policy_ready[env] = ready ? 1 : 0;
-    if (a.io.env_steps && type == 0) {   // env-steps executed: one atomic per wave
-      unsigned long long v = act ? n_stepped : 0;
-      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-      if (lane == 0 && v) atomicAdd(a.io.env_steps, v);
-    }
-  }
-  if (act) {
-    store_ship(a.st, sid, s);
-    a.st.nw[sid] = rt.nw;
-    for (int j = 0; j < lo_n; ++j) a.st.last_obs[(size_t)(lo_base + j) * n_env + env] = lo[j];
-    if (type == 1) {
-      a.st.env[0][env] = samp; a.st.env[1][env] = eps;
-      a.st.env[2][env] = ppn; a.st.env[3][env] = ppe;
-      a.st.env[4][env] = iwn; a.st.env[5][env] = iwe;
-      a.st.ep_step[env] = ep_step;
-      a.st.event[env] = event;
-      a.st.episodes[env] = episodes;
-    }
-  }
-#ifdef SIT_DIAG_PHASES
-  // whole-wave timing: [24] sum of wave cycles, [25] max wave cycles, [26] sum of prologue
-  // cycles, [27] sum of epilogue cycles, [28]/[29] min/max start (realtime), [30]/[31] min/max end
-  if (lane == 0) {
-    const unsigned long long w_t1 = __builtin_amdgcn_s_memtime();
-    const unsigned long long w_r1 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long* g = g_sit_diag[type];
-    atomicAdd(&g[24], w_t1 - w_t0);
-    atomicMax(&g[25], w_t1 - w_t0);
-    atomicAdd(&g[26], w_loop - w_t0 - (ph[0] + ph[1] + ph[2] + ph[3] + ph[4] + ph[5] + ph[6]));
-    atomicAdd(&g[27], w_t1 - w_loop);
-    atomicMin(&g[28], w_r0);
-    atomicMax(&g[29], w_r0);
-    atomicMin(&g[30], w_r1);
-    atomicMax(&g[31], w_r1);
-    const int wid = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
-    if (wid < kDiagWaves) {
-      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);     // HW_REG_HW_ID
-      const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);   // HW_REG_XCC_ID
-      g_sit_wave[wid][0] = w_r0; g_sit_wave[wid][1] = w_r1; g_sit_wave[wid][2] = w_t1 - w_t0;
-      g_sit_wave[wid][3] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
-    }
-  }
-#endif
-}
-
-// MultiShipRLEnv.init_step for masked envs (one thread per ship)
-template <typename T>
-__global__ __launch_bounds__(256) void k_init_step(const KArgs<T> a, const uint8_t* mask) {
-  const int sid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n_env = a.n_env;
-  if (sid >= 2 * n_env) return;
-  const int type = sid / n_env, env = sid - type * n_env;
-  if (mask && !mask[env]) return;
-  Ship<T> s;
-  load_ship(a.st, sid, s);
-  Route<T> rt;
-  rt.nw = a.st.nw[sid];
-  rt.end_n = a.sc.end_n[sid];
-  rt.end_e = a.sc.end_e[sid];
-  rt.tn = a.st.wn + (size_t)type * a.cap * n_env + env;
-  rt.te = a.st.we + (size_t)type * a.cap * n_env + env;
-  rt.stride = n_env;
-  rt.load_leg(s.k);
-  init_step_ship(a.c, s, rt, init_val(a.sc, type, SIT_INIT_DESIRED_SPEED, env, n_env));
-  store_ship(a.st, sid, s);
-}
-
-// MultiShipRLEnv.reset for masked envs (one thread per env)
-template <typename T>
-__global__ __launch_bounds__(256) void k_reset(const KArgs<T> a, const uint8_t* mask, T* initial_state) {
-  const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n_env = a.n_env;
-  if (env >= n_env) return;
-  if (!mask || mask[env]) {
-    for (int type = 0; type < 2; ++type) {
-      const int sid = type * n_env + env;
-      Ship<T> s;
-      load_ship(a.st, sid, s);
-      int nw;
-      reset_ship(a.sc, type, env, n_env, s, nw);
-      store_ship(a.st, sid, s);
-      a.st.nw[sid] = nw;
-    }
-    a.st.env[0][env] = T(0);
-    a.st.env[1][env] = T(0);
-    a.st.ep_step[env] = 0;
-    for (int j = 0; j < SIT_OBS_DIM; ++j)
-      a.st.last_obs[(size_t)j * n_env + env] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
-  }
-  // the construction-time observation (constant per env) is returned for every env
-  if (initial_state)
-    for (int j = 0; j < SIT_OBS_DIM; ++j)
-      initial_state[(size_t)env * SIT_OBS_DIM + j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
-}
-
-// map predicates of arbitrary points (test/diagnostic entry sit_probe_map, one thread per
-// point): boundary distance, Polygon.contains of the point, is_pos_inside_obstacles hull test
-template <typename T>
-__global__ __launch_bounds__(256) void k_probe_map(const KArgs<T> a, int n, const T* pts, T* dist,
-                                                   uint8_t* inside, uint8_t* hull) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const T pn = pts[2 * i], pe = pts[2 * i + 1];
-  const T d = distance_indexed(a.c, a.map, pn, pe);
-  if (dist) dist[i] = d;
-  if (inside) inside[i] = pip_point(a.c, a.map, pn, pe) ? 1 : 0;
-  if (hull) hull[i] = hull_in_terrain(a.c, a.map, pn, pe, d) ? 1 : 0;
-}
-
-// policy head + scatter (sit_policy_apply, one thread per request row): the squashed Gaussian
-// action tanh(mu + exp(clip(log_sigma, -20, 2)) * noise) (normal.py:88-101, gaussian_policy.py:
-// 71-72) of each queued env, written into its action slot and marked ready
-template <typename T>
-__global__ __launch_bounds__(256) void k_policy_apply(int cap, const T* head, int head_stride, const T* noise,
-                                                      const int32_t* req_env, const int32_t* req_count,
-                                                      int deterministic, T* policy_action, int32_t* policy_ready,
-                                                      int n_env) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cap || i >= *req_count) return;
-  const int e = req_env[i];
-  if (e < 0 || e >= n_env) return;
-  const T mu = head[(size_t)i * head_stride];
-  const T ls = xclip(head[(size_t)i * head_stride + 1], T(-20), T(2));
-  const T x = deterministic ? mu : mu + exp(ls) * noise[i];
-  policy_action[e] = tanh(x);
-  policy_ready[e] = 1;
-}
-
-// construction-time state (one thread per env)
-template <typename T>
-__global__ __launch_bounds__(256) void k_restart(const KArgs<T> a) {
-  const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n_env = a.n_env;
-  if (env >= n_env) return;
-  for (int type = 0; type < 2; ++type) {
-    const int sid = type * n_env + env;
-    Ship<T> s{};
-    int nw;
-    reset_ship(a.sc, type, env, n_env, s, nw);
-    s.w = init_val(a.sc, type, SIT_INIT_SHAFT_SPEED, env, n_env);
-    s.i1 = init_val(a.sc, type, SIT_INIT_SHIP_SPEED_I, env, n_env);
-    s.i2 = init_val(a.sc, type, SIT_INIT_SHAFT_SPEED_I, env, n_env);
-    s.hi = T(0); s.hp = T(0); s.lrpm = T(0); s.lect = T(0); s.lpme = T(0);
-    store_ship(a.st, sid, s);
-    a.st.nw[sid] = nw;
-  }
-  for (int j = 0; j < kEnvReal; ++j) a.st.env[j][env] = T(0);
-  a.st.ep_step[env] = 0;
-  a.st.event[env] = 0;
-  a.st.episodes[env] = 0;
-  for (int j = 0; j < SIT_OBS_DIM; ++j)
-    a.st.last_obs[(size_t)j * n_env + env] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
-}
-
-// =======================================================================================
-// host side
-// =======================================================================================
-struct sit_handle {
-  int precision = SIT_F32;
-  int n_env = 0;
-  int cap = 0;
-  int device = 0;
-  sit_params p{};
-  std::string err;
-  // state blob
-  unsigned char* blob = nullptr;
-  size_t blob_bytes = 0;
-  size_t off[kNumFields] = {};
-  int64_t count[kNumFields] = {};
-  // scenario
-  unsigned char* scen = nullptr;
-  size_t scen_init = 0, scen_end_n = 0, scen_end_e = 0, scen_nw0 = 0, scen_ab_len = 0,
-         scen_ab_alpha = 0, scen_initial = 0, scen_bytes = 0;
-  // map
-  unsigned char* map = nullptr;
-  int n_poly = 0, n_vert = 0;
-  size_t map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0, map_frank = 0, map_crec = 0, map_clive = 0;
-  int use_cells = 0;
-  int64_t n_mixed = 0, n_live = 0;
-  int lds_attr[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
-  size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
-  int use_index = 0;
-  double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
-  double fx0 = 0, fy0 = 0, finvx = 0, finvy = 0;
-  double min_n = 0, max_n = 0, min_e = 0, max_e = 0;
-  bool have_map = false, have_routes = false, have_init = false;
-};
-
+int sit_launch_steps_f32(sit_handle* h, const void* io, void* stream);   // sit_steps_f32.hip
 namespace {
-
-thread_local std::string g_create_err;
-
-int fail(sit_handle* h, int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  if (h) h->err = buf; else g_create_err = buf;
-  return code;
+int launch_steps_f32(sit_handle* h, const StepIO<float>& io, void* stream) {
+  return sit_launch_steps_f32(h, &io, stream);
 }
-
-#define HIP_TRY(h, call)                                                                    \
-  do {                                                                                      \
-    hipError_t e_ = (call);                                                                 \
-    if (e_ != hipSuccess) return fail((h), SIT_E_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
-  } while (0)
-
-size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
-size_t real_size(const sit_handle* h) { return h->precision == SIT_F64 ? 8 : 4; }
-
-// Derived constants, computed like the reference constructors (ship_model.py:71-130,
-// ship_engine.py:32-44, 316-325; controllers; MSRL_env_ex.py).
-template <typename T>
-Consts<T> make_consts(const sit_handle* h) {
-  const sit_params& p = h->p;
-  Consts<T> c{};
-  const double dwt = p.dead_weight_tonnage;
-  const double payload = 0.9 * (dwt - p.bunkers);
-  const double lsw = dwt / p.coefficient_of_deadweight_to_displacement - dwt;
-  const double mass = lsw + payload + p.bunkers + p.ballast;
-  const double l = p.length_of_ship, w = p.width_of_ship;
-  const double i_z = mass * (l * l + w * w) / 12;
-  const double x_du = mass * p.added_mass_coefficient_in_surge;
-  const double y_dv = mass * p.added_mass_coefficient_in_sway;
-  const double n_dr = i_z * p.added_mass_coefficient_in_yaw;
-  const double area_f = w * p.front_height, area_l = l * p.side_height;
-  c.dt = (T)p.integration_step;
-  c.mass = (T)mass; c.x_du = (T)x_du; c.y_dv = (T)y_dv;
-  c.inv_m11 = (T)(1.0 / (mass + x_du));
-  c.inv_m22 = (T)(1.0 / (mass + y_dv));
-  c.inv_m33 = (T)(1.0 / (i_z + n_dr));
-  c.d_u = (T)(mass / p.mass_over_linear_friction_coefficient_in_surge);
-  c.d_v = (T)(mass / p.mass_over_linear_friction_coefficient_in_sway);
-  c.d_r = (T)(i_z / p.mass_over_linear_friction_coefficient_in_yaw);
-  c.ku = (T)p.nonlinear_friction_coefficient_in_surge;
-  c.kv = (T)p.nonlinear_friction_coefficient_in_sway;
-  c.kr = (T)p.nonlinear_friction_coefficient_in_yaw;
-  c.vc_n = (T)p.current_velocity_component_from_north;
-  c.vc_e = (T)p.current_velocity_component_from_east;
-  c.wind_speed = (T)p.wind_speed;
-  c.wind_sin = (T)std::sin(p.wind_direction);
-  c.wind_cos = (T)std::cos(p.wind_direction);
-  c.wk_u = (T)(-0.5 * p.rho_air * p.cx * area_f);
-  c.wk_v = (T)(-0.5 * p.rho_air * p.cy * area_l);
-  c.wk_n = (T)(-p.rho_air * p.cn * area_l * l);
-  c.c_rv = (T)p.rudder_angle_to_sway_force_coefficient;
-  c.c_rr = (T)p.rudder_angle_to_yaw_force_coefficient;
-  c.rudder_max = (T)(p.max_rudder_angle_degrees * M_PI / 180);
-  const double me = p.main_engine_capacity, el = p.electrical_capacity, hotel = p.hotel_load;
-  double avail = 0, avail_me = 0, avail_el = 0;
-  if (hotel != 0.0) {   // BaseMachineryModel only sets the powers for a truthy hotel load
-    if (p.shaft_generator_state == SIT_SG_MOTOR) { avail = me + el - hotel; avail_me = me; avail_el = el - hotel; }
-    else if (p.shaft_generator_state == SIT_SG_GEN) { avail = me - hotel; avail_me = me - hotel; avail_el = 0; }
-    else { avail = me; avail_me = me; avail_el = 0; }
-  }
-  c.avail_prop = (T)avail; c.avail_me = (T)avail_me; c.avail_el = (T)avail_el;
-  c.tqcap_me = (T)(avail_me / 5 * M_PI / 30);
-  c.tqcap_el = (T)(avail_el / 5 * M_PI / 30);
-  c.d_me = (T)p.linear_friction_main_engine;
-  c.d_hsg = (T)p.linear_friction_hybrid_shaft_generator;
-  c.r_me = (T)p.gear_ratio_between_main_engine_and_propeller;
-  c.r_hsg = (T)p.gear_ratio_between_hybrid_shaft_generator_and_propeller;
-  c.kp_prop = (T)p.propeller_speed_to_torque_coefficient;
-  c.jp = (T)p.propeller_inertia;
-  c.thrust_k = (T)(std::pow(p.propeller_diameter, 4.0) * p.propeller_speed_to_thrust_force_coefficient);
-  c.me_cap = (T)me; c.hotel = (T)hotel; c.load_el_gen = (T)std::min(hotel, el);
-  c.sg_mode = p.shaft_generator_state;
-  c.collision_bias = p.collision_bias;
-  c.kp1 = (T)p.kp_ship_speed; c.ki1 = (T)p.ki_ship_speed;
-  c.kp2 = (T)p.kp_shaft_speed; c.ki2 = (T)p.ki_shaft_speed;
-  c.kp_h = (T)p.heading_kp; c.kd_h = (T)p.heading_kd; c.ki_h = (T)p.heading_ki;
-  c.los_r = (T)p.lookahead_distance;
-  c.los_r2 = (T)(p.lookahead_distance * p.lookahead_distance);
-  c.los_clamp = (T)(0.99 * p.lookahead_distance);
-  c.los_ki = (T)p.los_integral_gain;
-  c.windup = (T)p.integrator_windup_limit;
-  c.ra2 = p.radius_of_acceptance * p.radius_of_acceptance;
-  c.bias_scale = (T)p.bias_throttle_scale;
-  c.bias_max = (T)p.bias_throttle_max;
-  c.bias_rudder = (T)(p.bias_rudder_degrees * (M_PI / 180.0));
-  c.e_tol = (T)p.e_tolerance;
-  c.arrival_radius = (T)p.arrival_radius;
-  c.rpm_max = (T)p.shaft_rpm_max;
-  c.min_dist2 = (T)(p.minimum_ship_distance * p.minimum_ship_distance);
-  c.theta = (T)p.theta;
-  c.blackout_kw = (T)(me / 1000);
-  c.rpm_k = (T)(30.0 / M_PI);
-  c.inv_dt = (T)(1.0 / p.integration_step);
-  c.inv_e_tol = (T)(1.0 / p.e_tolerance);
-  c.inv_maxn = (T)(1.0 / h->max_n);
-  c.inv_jp = (T)(1.0 / p.propeller_inertia);
-  c.inv_r_me = (T)(1.0 / p.gear_ratio_between_main_engine_and_propeller);
-  c.inv_r_hsg = (T)(1.0 / p.gear_ratio_between_hybrid_shaft_generator_and_propeller);
-  c.half_len = (T)(l / 2);
-  c.min_n = (T)h->min_n; c.max_n = (T)h->max_n; c.min_e = (T)h->min_e; c.max_e = (T)h->max_e;
-  c.pi6 = (T)(M_PI / 6.0);
-  c.gx0 = (T)h->gx0; c.gy0 = (T)h->gy0; c.ginvx = (T)h->ginvx; c.ginvy = (T)h->ginvy;
-  c.by0 = (T)h->by0; c.binv = (T)h->binv;
-  c.hull_safe = (T)(l / 2 * std::sqrt(2.0) + 1.0);
-  c.fx0 = (T)h->fx0; c.fy0 = (T)h->fy0; c.finvx = (T)h->finvx; c.finvy = (T)h->finvy;
-  c.el_cap = (T)el;
-  c.fuel_me_a = (T)p.fuel_me_a; c.fuel_me_b = (T)p.fuel_me_b; c.fuel_me_c = (T)p.fuel_me_c;
-  c.fuel_dg_a = (T)p.fuel_dg_a; c.fuel_dg_b = (T)p.fuel_dg_b; c.fuel_dg_c = (T)p.fuel_dg_c;
-  c.rad2deg = (T)(180.0 / M_PI);
-  return c;
+#else   // single-TU build (diagnostic builds): float32 step kernels compiled here, strict fp
+int launch_steps_f32(sit_handle* h, const StepIO<float>& io, void* stream) {
+  return launch_steps<float>(h, io, (hipStream_t)stream);
 }
-
-template <typename T>
-KArgs<T> make_args(const sit_handle* h) {
-  KArgs<T> a{};
-  a.c = make_consts<T>(h);
-  a.n_env = h->n_env;
-  a.cap = h->cap;
-  auto fp = [&](int f) { return reinterpret_cast<T*>(h->blob + h->off[f]); };
-  auto ip = [&](int f) { return reinterpret_cast<int32_t*>(h->blob + h->off[f]); };
-  for (int i = 0; i < kShipReal; ++i) a.st.ship[i] = fp(F_NORTH + i);
-  a.st.k = ip(F_K); a.st.nw = ip(F_NW); a.st.ticks = ip(F_TICKS); a.st.stop = ip(F_STOP);
-  for (int i = 0; i < kEnvReal; ++i) a.st.env[i] = fp(F_SAMP + i);
-  a.st.ep_step = ip(F_EP);
-  a.st.event = reinterpret_cast<uint32_t*>(h->blob + h->off[F_EVENT]);
-  a.st.episodes = reinterpret_cast<uint32_t*>(h->blob + h->off[F_EPISODES]);
-  a.st.wn = fp(F_WN); a.st.we = fp(F_WE);
-  a.st.last_obs = fp(F_LAST_OBS);
-  for (int i = 0; i < 3; ++i) a.st.fuel[i] = fp(F_FUEL_ME + i);
-  a.st.last_log = fp(F_LAST_LOG);
-  a.sc.init = reinterpret_cast<const T*>(h->scen + h->scen_init);
-  a.sc.end_n = reinterpret_cast<const T*>(h->scen + h->scen_end_n);
-  a.sc.end_e = reinterpret_cast<const T*>(h->scen + h->scen_end_e);
-  a.sc.nw0 = reinterpret_cast<const int32_t*>(h->scen + h->scen_nw0);
-  a.sc.ab_len = reinterpret_cast<const double*>(h->scen + h->scen_ab_len);
-  a.sc.ab_alpha = reinterpret_cast<const double*>(h->scen + h->scen_ab_alpha);
-  a.sc.initial_state = reinterpret_cast<const T*>(h->scen + h->scen_initial);
-  a.map.n_poly = h->n_poly;
-  a.map.n_edge = h->n_vert;
-  a.map.use_index = h->use_index;
-  a.map.edge = reinterpret_cast<const Edge<T>*>(h->map);
-  a.map.idx = reinterpret_cast<const uint16_t*>(h->map + h->map_idx);
-  a.map.fine = reinterpret_cast<const uint32_t*>(h->map + h->map_fine);
-  a.map.frank = reinterpret_cast<const uint16_t*>(h->map + h->map_frank);
-  a.map.crec = reinterpret_cast<const uint2*>(h->map + h->map_crec);
-  a.map.clive = reinterpret_cast<const uint8_t*>(h->map + h->map_clive);
-  a.map.use_cells = h->use_cells;
-  a.map.off = reinterpret_cast<const int32_t*>(h->map + h->map_off);
-  a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
-  a.map_bytes = (int32_t)h->map_bytes;
-  return a;
-}
-
-int ready(sit_handle* h) {
-  if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
-  if (!h->have_map) return fail(h, SIT_E_STATE, "sit_load_map has not been called");
-  if (!h->have_routes) return fail(h, SIT_E_STATE, "sit_load_routes has not been called");
-  if (!h->have_init) return fail(h, SIT_E_STATE, "sit_load_initial has not been called");
-  return SIT_OK;
-}
-
-// LDS budget of one step-kernel block: two blocks (4 waves, one per SIMD) must fit the CU's
-// 160 KB; above 80 KB only one block fits and the grid runs in two rounds (~1.75x slower)
-constexpr size_t kLdsBudget = 80 * 1024;
-size_t map_lds_bytes(const sit_handle* h) { return (h->map_bytes + 255) & ~size_t(255); }
-
-template <typename T>
-int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
-  KArgs<T> a = make_args<T>(h);
-  a.io = io;
-  const int blocks = (h->n_env + kEnvsPerBlock - 1) / kEnvsPerBlock;
-  const int mode = io.action_ne ? kExplicit : (io.policy_action ? kPolicy : kSynth);
-  // the map (edges, index, classes) is staged in LDS when it fits the budget next to the
-  // static exchange buffers; otherwise the predicates read it through the caches
-  const size_t stat = sizeof(Xchg<T>) * 2 + sizeof(Consts<T>) + 256;
-  const bool lds_map = map_lds_bytes(h) + stat <= kLdsBudget;
-  const size_t lds = lds_map ? map_lds_bytes(h) : 0;
-  auto go = [&](auto kern) -> int {
-    // the dynamic-LDS attribute is set once per kernel and size (not per launch: launches may be
-    // captured into HIP graphs)
-    const int slot = (mode * 2 + (lds_map ? 1 : 0)) * 2 + (io.log ? 1 : 0);
-    if (lds_map && h->lds_attr[slot] != (int)lds) {
-      HIP_TRY(h, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      h->lds_attr[slot] = (int)lds;
-    }
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(128), lds, stream, a);
-    return SIT_OK;
-  };
-  auto pick = [&](auto mode_tag) -> int {
-    constexpr int M = decltype(mode_tag)::value;
-    if (io.log) return lds_map ? go(k_env_steps<T, M, true, true>) : go(k_env_steps<T, M, false, true>);
-    return lds_map ? go(k_env_steps<T, M, true, false>) : go(k_env_steps<T, M, false, false>);
-  };
-  int rc;
-  if (mode == kSynth) rc = pick(std::integral_constant<int, kSynth>{});
-  else if (mode == kPolicy) rc = pick(std::integral_constant<int, kPolicy>{});
-  else rc = pick(std::integral_constant<int, kExplicit>{});
-  if (rc) return rc;
-  HIP_TRY(h, hipGetLastError());
-  return SIT_OK;
-}
+#endif
 
 }  // namespace
 
@@ -1790,7 +622,7 @@ int sit_step(sit_handle* h, const void* action_ne, const uint8_t* sac_update, co
   io.n_steps = 1; io.action_ne = (const float*)action_ne; io.sac_update = sac_update; io.init = init;
   io.next_state = (float*)next_state; io.reward = (float*)reward; io.done = done; io.status = status;
   io.done_count = done_count;
-  return launch_steps<float>(h, io, (hipStream_t)stream);
+  return launch_steps_f32(h, io, stream);
 }
 
 int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
@@ -1835,7 +667,7 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
   }
   StepIO<float> io{};
   fill(&io, (float*)nullptr);
-  return launch_steps<float>(h, io, (hipStream_t)stream);
+  return launch_steps_f32(h, io, stream);
 }
 
 int sit_state_field(const sit_handle* h, int32_t id, const char** name, size_t* offset, int32_t* dtype,
