@@ -92,10 +92,13 @@ struct Consts {
 // LDS base pointer, immediate field offsets) so the predicates need no per-array registers.
 //
 // Spatial index (built on the host by sit_load_map, exact by construction), one u16 array:
-//   idx[0 .. 2*G*G)          grid cell records, one u32 each: first group (in 8-byte groups
-//                            from the start of idx) | group count << 16
+//   idx[0 .. 4*G*G)          grid cell records, 8 bytes each: the list's first group inline
+//                            (x = ids 0-3, y bits 0-7 = id 4), y bits 8-15 = number of further
+//                            groups, y bits 16-31 = the first of them (in 8-byte groups from the
+//                            start of idx).  The cell's first 5 candidates are then one LDS read
+//                            away from the cell index, their edges two.
 //   idx[kBandBase ..]        NB+1 band starts (absolute positions in idx)
-//   then the band entries (edge ids), then the grid groups (8-byte aligned).
+//   then the band entries (edge ids), then the further grid groups (8-byte aligned).
 //  * grid: G x G cells over the map extent plus a margin; cell c lists every edge that can be
 //    the nearest edge of some point within 1 m of the cell (conservative prefilter, then a
 //    Lipschitz-sampled refinement with a 1 m float slack; sit_load_map), so the minimum over the
@@ -111,7 +114,7 @@ struct Consts {
 //    ~31 m from the shore resolves by one lookup.
 constexpr int kGrid = 32;
 constexpr int kBands = 64;
-constexpr int kBandBase = 2 * kGrid * kGrid;
+constexpr int kBandBase = 4 * kGrid * kGrid;
 constexpr int kIdxHead = kBandBase + kBands + 1;
 constexpr int kFine = 256;
 constexpr int kFineWords = kFine * kFine / 16;
@@ -541,17 +544,16 @@ __device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   if (!m.use_index || !(fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)))
     return distance_to_polys(m, n, e);
   const int cell = (int)fy * kGrid + (int)fx;
-  const uint32_t rec = reinterpret_cast<const uint32_t*>(m.idx)[cell];
-  const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (rec & 0xffffu);
-  const int ng = (int)(rec >> 16);
-  // every list has >= 1 group (5 u8 ids in 8 bytes, padded by repetition); the first is unrolled
-  // so its loads issue without a loop branch in front of them
-  uint2 q = grp[0];
+  // every list has >= 1 group (5 u8 ids in 8 bytes, padded by repetition); the first sits in the
+  // cell record, so its edge loads depend on a single LDS read
+  uint2 q = reinterpret_cast<const uint2*>(m.idx)[cell];
+  const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (q.y >> 16);
+  const int ng = (int)((q.y >> 8) & 0xffu);
   T best = xmin(xmin(xmin(edge_dist2(m.edge[q.x & 0xffu], e, n), edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n)),
                      xmin(edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n), edge_dist2(m.edge[q.x >> 24], e, n))),
                 edge_dist2(m.edge[q.y & 0xffu], e, n));
 #pragma unroll 1
-  for (int g = 1; g < ng; ++g) {
+  for (int g = 0; g < ng; ++g) {
     q = grp[g];
     const T d0 = edge_dist2(m.edge[q.x & 0xffu], e, n);
     const T d1 = edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n);

@@ -153,8 +153,14 @@ template <typename T>
 __device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* dst) {
   const unsigned char* src = reinterpret_cast<const unsigned char*>(a.map.edge);
   const int n16 = a.map_bytes / 16;
+  // LDS-DMA (global_load_lds_dwordx4): the 16-byte pieces go global -> LDS without a register
+  // round trip, so all of a thread's pieces are in flight at once instead of one load latency
+  // per piece.  One wave-instruction writes a wave-uniform base + lane x 16 B: the linear image.
+  // The barrier after the prologue waits for them (vmcnt).
+  const int lane = threadIdx.x & (kWave - 1);
   for (int i = threadIdx.x; i < n16; i += blockDim.x)
-    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(src) + i,
+                                     (__attribute__((address_space(3))) void*)(dst + 16 * (i - lane)), 16, 0, 0);
   Map<T> m = a.map;
   m.edge = reinterpret_cast<const Edge<T>*>(dst);
   m.idx = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.idx) - src));
@@ -292,7 +298,7 @@ __device__ void diag_lane(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst
   const T fx = (e - c.gx0) * c.ginvx, fy = (n - c.gy0) * c.ginvy;
   if (m.use_index && fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid)) {
     const int cell = (int)fy * kGrid + (int)fx;
-    v[0] = (int)(reinterpret_cast<const uint32_t*>(m.idx)[cell] >> 16) * 5;
+    v[0] = (int)(((reinterpret_cast<const uint2*>(m.idx)[cell].y >> 8) & 0xffu) + 1u) * 5;
   }
   if (dobst <= c.hull_safe) {
     v[1] = 1;

@@ -417,21 +417,34 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     }
   }
   const bool cells_ok = crec.size() / 2 <= 65535 && clive.size() <= 65535;
+  // each cell's first group goes into its record; the further groups (lists of > 5) follow the
+  // band entries
+  std::vector<uint16_t> grest;
+  std::vector<uint32_t> rstart(kGrid * kGrid);
+  for (int c = 0; c < kGrid * kGrid; ++c) {
+    rstart[c] = (uint32_t)grest.size();
+    grest.insert(grest.end(), gentries.begin() + gstart[c] + 4, gentries.begin() + gstart[c + 1]);
+  }
   const size_t head = (size_t)kIdxHead;
   const size_t gbase = (head + bentries.size() + 3) & ~size_t(3);   // 8-byte aligned groups
-  const size_t n_idx = gbase + gentries.size();
+  const size_t n_idx = gbase + grest.size();
   h->use_index = (n_idx < 65535 && n_idx * 2 <= 48 * 1024) ? 1 : 0;
   h->gx0 = gx0; h->gy0 = gy0; h->ginvx = 1.0 / sx; h->ginvy = 1.0 / sy;
   h->by0 = by0; h->binv = 1.0 / bh;
-  std::vector<uint16_t> idx(h->use_index ? n_idx : 2, 0);
+  std::vector<uint16_t> idx(h->use_index ? n_idx : 4, 0);
   if (h->use_index) {
     for (int c = 0; c < kGrid * kGrid; ++c) {
-      idx[2 * c] = (uint16_t)((gbase + gstart[c]) / 4);             // first group
-      idx[2 * c + 1] = (uint16_t)((gstart[c + 1] - gstart[c]) / 4); // group count
+      const uint16_t* f = gentries.data() + gstart[c];
+      const uint32_t more = (gstart[c + 1] - gstart[c]) / 4 - 1;    // < 52: ids are u8, 5 per group
+      const uint32_t y = (f[2] & 0xffu) | (more << 8) | ((uint32_t)((gbase + rstart[c]) / 4) << 16);
+      idx[4 * c] = f[0];                       // ids 0, 1
+      idx[4 * c + 1] = f[1];                   // ids 2, 3
+      idx[4 * c + 2] = (uint16_t)(y & 0xffffu);
+      idx[4 * c + 3] = (uint16_t)(y >> 16);
     }
     for (int b = 0; b <= kBands; ++b) idx[kBandBase + b] = (uint16_t)(head + bstart[b]);
     std::copy(bentries.begin(), bentries.end(), idx.begin() + head);
-    std::copy(gentries.begin(), gentries.end(), idx.begin() + gbase);
+    std::copy(grest.begin(), grest.end(), idx.begin() + gbase);
   }
   // blob: [Edge<T>[nv]][u16 index][u32 classes] (staged into LDS) [ring offsets][bboxes] (fallback, global)
   const size_t esz = rs == 8 ? sizeof(Edge<double>) : sizeof(Edge<float>);
