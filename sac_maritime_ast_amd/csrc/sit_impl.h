@@ -250,6 +250,21 @@ struct Xchg {
   int32_t slot[kWave];    // transition record of this step (obstacle lane allocates)
 };
 
+// the action row's angle: the sampled a, or NaN when none was drawn on device.  The float32 step
+// kernels are compiled with finite math, under which a NaN literal or a select against one may be
+// folded away; the NaN bit pattern therefore passes an empty asm, which the optimiser cannot see
+// through (tests/test_gpu_parity.py::test_f32_action_rows_nan_without_sample)
+__device__ __forceinline__ float angle_or_nan(bool has, float a) {
+  uint32_t nan_bits = 0x7fc00000u;
+  asm volatile("" : "+v"(nan_bits));
+  return __uint_as_float(has ? __float_as_uint(a) : nan_bits);
+}
+__device__ __forceinline__ double angle_or_nan(bool has, double a) {
+  uint64_t nan_bits = 0x7ff8000000000000ull;
+  asm volatile("" : "+v"(nan_bits));
+  return __longlong_as_double(has ? __double_as_longlong(a) : (long long)nan_bits);
+}
+
 // ---------------------------------------------------------------------------------------
 // the env step kernel: K steps of MultiShipRLEnv.step (+ optional auto-reset)
 //   MODE  : kExplicit = caller's action arrays, kSynth = synthetic AST sampler on device,
@@ -489,7 +504,8 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     int dv[7] = {0, 0, 0, 0, 0, 0, 0};
 #endif
     bool sac = false, init_f = false;
-    double ang = NAN;
+    double ang = 0.0;                  // the sampled angle; has_ang: drawn on device this step
+    bool has_ang = false;
     bool stall_now = false;
     if (MODE == kPolicy && act && !stalled && need && !ready) {
       // sampling event without an action: wait for the policy; the obstacle lane queues the
@@ -518,6 +534,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           sac = need;
           if (sac) {                     // the policy's squashed action scales the route angle
             ang = (double)pa * (M_PI / 6.0);
+            has_ang = true;
             iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
             ++event;
           }
@@ -527,6 +544,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           if (sac) {
             const double u01 = sampler_uniform(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
             ang = (u01 * 2.0 - 1.0) * (M_PI / 6.0);
+            has_ang = true;
             iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
             ++event;
           }
@@ -733,13 +751,13 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         if (outs & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_ect); }
 #endif
 #ifndef SIT_ABLATE_STORES
-        if (outs & 16) { store2(p_ao, iwn, iwe); store2(p_ao + 2, (T)ang, sac ? T(1) : T(0)); }
+        if (outs & 16) { store2(p_ao, iwn, iwe); store2(p_ao + 2, angle_or_nan(has_ang, (T)ang), sac ? T(1) : T(0)); }
 #endif
         const int slot = x.slot[lane];
         if (slot >= 0 && slot < a.io.transition_capacity) {
           T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
           for (int j = 0; j < 4; ++j) rec[6 + j] = lo[j];
-          rec[10] = (T)ang;
+          rec[10] = angle_or_nan(has_ang, (T)ang);
           rec[18] = s.n; rec[19] = s.e; rec[20] = s.psi; rec[21] = o_ect;
           if (MODE == kPolicy) rec[10] = pa;   // the policy's action (memory.push, main_ast.py:395)
           rec[23] = (T)(a.io.env_id_offset + env);

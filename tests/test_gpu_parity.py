@@ -321,6 +321,21 @@ def test_f32_sampler_iw_vs_oracle():
     assert err.max() <= 1e-5, f"IW rel err {err.max():.3e}"
 
 
+def test_f32_action_rows_nan_without_sample():
+    """The float32 step kernels run with finite math: the action row's angle must
+    still be NaN exactly on the rows without a sampling event, and finite on the others."""
+    n_env = 2048
+    env = VecMultiShipRLEnv(scenario=make_scenario(n_env, cap=48), precision=32, device=DEV)
+    env.reset()
+    env.init_step()
+    out = env.rollout(300, seed=11)
+    a = out["action"].cpu().numpy()
+    sac = a[..., 3] > 0.5
+    assert sac.any() and (~sac).any()
+    assert np.isnan(a[..., 2][~sac]).all()
+    assert np.isfinite(a[..., 2][sac]).all() and np.abs(a[..., 2][sac]).max() <= np.pi / 6 + 1e-6
+
+
 # ------------------------------------------------------------------------------------------
 # trajectory logs (simulation_results rows, fuel model, reward_results terms)
 # ------------------------------------------------------------------------------------------
