@@ -19,6 +19,7 @@ import argparse
 import glob
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -51,6 +52,8 @@ def parse():
     ap.add_argument("--request-div", type=int, default=4, help="policy mode: request capacity = envs / this")
     ap.add_argument("--graph-launches", type=int, default=16, help="policy mode: launches per HIP graph")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-baseline-workers", type=int, default=16,
+                    help="single-threaded oracle processes (the GPU box's CPU share is 16 cores per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--launch-trace", action="store_true", help="print every launch's kernel ms to stderr")
@@ -89,25 +92,62 @@ def latest_pmc(precision, mode, n_env, chunk):
     return best
 
 
-def cpu_baseline(seconds, seed):
-    """The oracle (float64 NumPy restatement, vectorised over envs, 1 core) on a bounded sample of
-    the same workload: 2048 envs, synthetic sampler, auto-reset, until ~`seconds` of CPU work."""
-    from oracle import sit_oracle as so  # CPU baseline leg only
-    from sac_maritime_ast_amd.scenario import make_scenario
+CPU_WORKER = r"""
+import json, sys, time
+sys.path.insert(0, sys.argv[1])
+from oracle import sit_oracle as so  # CPU baseline leg only
+from sac_maritime_ast_amd.scenario import make_scenario
+n_env, seconds, seed, part = int(sys.argv[2]), float(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+sc = make_scenario(n_env, cap=32, seed=seed, env_offset=part * n_env)
+o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+o.reset()
+o.init_step()
+o.rollout(2, seed, env_id_offset=part * n_env)
+steps, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < seconds:
+    o.rollout(10, seed, env_id_offset=part * n_env)
+    steps += 10
+print(json.dumps({"env_steps": n_env * steps, "steps": steps, "seconds": time.perf_counter() - t0}))
+"""
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds, seed, workers):
+    """The oracle (float64 NumPy restatement, vectorised over envs) on a bounded sample of the same
+    workload: per worker process 2048 envs (its own global env-id range), synthetic sampler,
+    auto-reset, ~`seconds` of CPU work; `workers` single-threaded processes on the host cores
+    (one process per core).  Workers are fresh interpreters started as child
+    processes (nothing of this GPU process is forked into them); value = the env-steps all workers
+    did / the slowest worker's time."""
     n_env = 2048
-    sc = make_scenario(n_env, cap=32)
-    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
-    o.reset()
-    o.init_step()
-    o.rollout(2, seed)
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        o.rollout(10, seed)
-        steps += 10
-    dt = time.perf_counter() - t0
-    return {"value": n_env * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/sit_oracle.py float64 NumPy, {n_env} envs x {steps} steps (synthetic "
-                      f"sampler, auto-reset), {dt:.1f} s on 1 host core"}
+    cores = max(1, min(workers, len(os.sched_getaffinity(0))))
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1",
+               PYTHONDONTWRITEBYTECODE="1")
+    procs = [subprocess.Popen([sys.executable, "-c", CPU_WORKER, ROOT, str(n_env), str(seconds), str(seed), str(p)],
+                              stdout=subprocess.PIPE, env=env, text=True) for p in range(cores)]
+    res = []
+    for p in procs:
+        outp, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError(f"cpu baseline worker failed (exit {p.returncode})")
+        res.append(json.loads(outp.strip().splitlines()[-1]))
+    total = sum(r["env_steps"] for r in res)
+    dt = max(r["seconds"] for r in res)
+    return {"value": total / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "per_core_value": float(np.mean([r["env_steps"] / r["seconds"] for r in res])),
+            "cpu_model": _cpu_model(),
+            "sample": f"oracle/sit_oracle.py float64 NumPy, {cores} single-threaded processes x {n_env} envs x "
+                      f"~{int(np.mean([r['steps'] for r in res]))} steps each (synthetic sampler, auto-reset), "
+                      f"{dt:.1f} s wall"}
 
 
 def stats_of(launch_ms):
@@ -334,7 +374,7 @@ def main():
               "data": "synthetic (SURVEY §8(d) routes, island map of test_policy.py:189-194, Philox random IWs)",
               "config": r["config"], "roofline": r["roofline"]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.seed)
+        result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.seed, args.cpu_baseline_workers)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
