@@ -42,7 +42,7 @@ def parse():
                     "starts synchronised; ~40k steps reach the steady state of desynchronised episodes)")
     ap.add_argument("--n-env", type=int, default=32768, help="two-ship envs per GPU (32768 = 64k ships)")
     ap.add_argument("--chunk", type=int, default=None,
-                    help="env steps fused per kernel launch (default 1000; 32 in policy mode)")
+                    help="env steps fused per kernel launch (default 5000; 32 in policy mode)")
     ap.add_argument("--precision", type=int, default=32, choices=(32, 64))
     ap.add_argument("--seed", type=int, default=25450)
     ap.add_argument("--mode", default="rollout", choices=("rollout", "step", "policy"),
@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--launch-trace", action="store_true", help="print every launch's kernel ms to stderr")
     args = ap.parse_args()
     if args.chunk is None:
-        args.chunk = 32 if args.mode == "policy" else 1000
+        args.chunk = 32 if args.mode == "policy" else 5000
     return args
 
 
