@@ -5,12 +5,12 @@ args=()
 for lib in "$@"; do
   n=$(basename $lib .so)
   args+=("$n" 120 env SIT_LIBRARY=$lib python bench.py --no-cpu-baseline --warmup 40000 --steps 20000 --chunk 200 "---")
-  args+=("${n}_c1000" 120 env SIT_LIBRARY=$lib python bench.py --no-cpu-baseline --warmup 40000 --steps 20000 --chunk 1000 "---")
+  args+=("${n}_c5000" 120 env SIT_LIBRARY=$lib python bench.py --no-cpu-baseline --warmup 40000 --steps 20000 --chunk 5000 "---")
 done
 tools/gpu_steps.sh "${args[@]}"
 for lib in "$@"; do
   n=$(basename $lib .so)
-  for f in $n ${n}_c1000; do
+  for f in $n ${n}_c5000; do
     python -c "
 import json
 for l in open('gpurun_out/$f.log'):
