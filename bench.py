@@ -209,7 +209,9 @@ def bench_rollout(args, rank, world, dev):
     stream = torch.cuda.current_stream(dev)
     # replay transitions of sampling events: written by the kernel with a device-side count and
     # all-gathered over RCCL once per launch (no host synchronisation)
-    tcap = max(1024, n_env * chunk // 64)
+    # capacity: measured steady-state rate 1 transition per ~390 env-steps (C3, K = 5000, launch 0:
+    # 1 per 369; tools/tcount.py), so 1 per 192 leaves 2x headroom (overflow is counted, not written)
+    tcap = max(1024, n_env * chunk // 192)
     gather = AsyncTransitionGather(tcap, 24, env.dtype, dev, world) if (world > 1 and not args.no_gather) else None
     out = {}
     launch_no = [0]
