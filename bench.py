@@ -8,10 +8,20 @@ Config C3: 65 536 ships = 32 768 two-ship envs per GPU (weak scaling over ranks)
 fused launches of --chunk steps; every step's full output (next_state[10], reward, done,
 status, IW action) is written to HBM.  Inputs (env state) are resident in HBM before timing.
 
-Multi-GPU: one process per GPU (torchrun); each rank owns an independent env shard (global
-env ids offset by rank, no data-path collective) and, once per chunk, the replay transitions
-of that chunk's sampling events (the only data the SAC learner consumes, test_beds/main_ast.py:
-395-396) are compacted on device and all-gathered over RCCL to every rank (rank 0 = learner).
+Multi-GPU: one process per GPU.  ``bench.py --gpus N`` started without torchrun's environment
+re-launches itself under ``torch.distributed.run`` (N rank processes, 127.0.0.1 rendezvous)
+before anything touches a GPU; under torchrun (WORLD_SIZE set) --gpus must equal WORLD_SIZE.
+Each rank owns an independent env shard (global env ids offset by rank, no data-path
+collective); per launch the replay transitions of its sampling events (the only data the SAC
+learner consumes, test_beds/main_ast.py:395-396) go to rank 0 (the learner) over RCCL: the
+per-rank counts are all-gathered, then exactly the valid records move point-to-point
+(sac_maritime_ast_amd/shard.py).
+
+Timing: W warm-up steps (at least 8 launches: the env population starts synchronised and needs
+~40 000 steps to reach the steady state of desynchronised episodes), then K timed steps in
+whole launches (at least 3), bracketed by barrier + synchronize, max over ranks.  A "step" is one
+env step of every env; with --steps below 3 launches the used count is reported beside the
+requested one.
 """
 from __future__ import annotations
 
@@ -40,6 +50,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20000)
     ap.add_argument("--warmup", type=int, default=40000, help="steps before timing (the env population "
                     "starts synchronised; ~40k steps reach the steady state of desynchronised episodes)")
+    ap.add_argument("--min-launches", type=int, default=3, help="timed launches at least")
+    ap.add_argument("--min-warmup-launches", type=int, default=8, help="warm-up launches at least")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/collective self-check without a GPU (gloo, CPU tensors, synthetic records)")
     ap.add_argument("--n-env", type=int, default=32768, help="two-ship envs per GPU (32768 = 64k ships)")
     ap.add_argument("--chunk", type=int, default=None,
                     help="env steps fused per kernel launch (default 5000; 32 in policy mode)")
@@ -155,26 +169,56 @@ def stats_of(launch_ms):
     return {"min": float(v.min()), "median": float(np.median(v)), "max": float(v.max())}
 
 
-def setup_dist():
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """--gpus N without torchrun's environment: run this script as N rank processes under
+    torch.distributed.run (a child process, started before anything here touched a GPU), and
+    return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def setup_dist(args):
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch with --gpus equal to the "
+                         f"number of rank processes (or without torchrun: bench.py starts them itself)")
+    if args.dry_run:
+        dev = torch.device("cpu")
+        if world > 1:
+            torch.distributed.init_process_group("gloo")
+        return rank, world, dev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        torch.distributed.init_process_group("nccl", device_id=dev)
     return rank, world, dev
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
 
 
 def timed(dev, world, fn):
     """Barrier + synchronize on both sides of fn(); max over ranks of the wall time."""
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
     fn()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
@@ -184,12 +228,73 @@ def timed(dev, world, fn):
     return float(t.item())
 
 
+def dry_run(args, rank, world, dev):
+    """The multi-rank skeleton of bench_rollout on CPU (gloo): the same launcher, shard offsets,
+    pipelined transition gather to the learner and max-over-ranks timing, with synthetic records
+    (rank r writes 3 + launch + r records per launch) instead of the GPU kernel."""
+    from sac_maritime_ast_amd.shard import AsyncTransitionGather, shard_offset
+    cap = 64
+    g = AsyncTransitionGather(cap, 24, torch.float64, dev, world)
+    n_launch = max(args.min_launches, 3)
+    got = []
+
+    def run():
+        for i in range(n_launch):
+            rec, cnt = g.buffers(i)
+            n = 3 + i + rank
+            rec.zero_()
+            rec[:n, 0] = float(i)
+            rec[:n, 23] = float(shard_offset(rank, 1000) + rank)
+            cnt.fill_(n)
+            g.start(i)
+            g.progress(i - 1)
+            if rank == 0 and i > 0:
+                got.append(int(g.records(i - 1).shape[0]))
+        g.finish()
+        if rank == 0:
+            got.append(int(g.records(n_launch - 1).shape[0]))
+    elapsed = timed(dev, world, run)
+    want = [sum(3 + i + r for r in range(world)) for i in range(n_launch)]
+    return {"dry_run": True, "n_gpus": world, "world_size": world, "launches": n_launch, "seconds": elapsed,
+            "gathered": g.gathered, "dropped": g.dropped(), "records_per_launch_ok": got == want if rank == 0 else None}
+
+
 def roofline(alg_bytes, kern_ms, pmc):
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": (pmc["hbm_bytes_per_launch"] if pmc else None),
             "kernel": "k_env_steps", "kernel_ms_per_launch": kern_ms,
             "algorithmic_bytes_per_launch": alg_bytes}
+
+
+# VALU issue peak of the chip: 256 CUs x 4 SIMD-32 x one wave64 VALU instruction per 2 cycles at
+# 2.4 GHz (MI355X_MICROARCH.md: v_fma_f32 2 cyc/SIMD; one wave alone issues at most every 4)
+VALU_PEAK_INST_S = 256 * 4 * 2.4e9 / 2
+
+
+def roofline_valu(kern_ms, pmc, n_env, chunk):
+    """The kernel's binding resource: wave64 VALU instructions issued per second
+    against the chip's VALU issue peak.  Instructions per launch from the committed rocprofv3 PMC
+    summary of this launch configuration (SQ_INSTS_VALU), time from this run's HIP events."""
+    per = (pmc or {}).get("per_wave_step", {}).get("SQ_INSTS_VALU")
+    if per is None:
+        return {"bound": "valu-issue", "achieved": None, "peak": VALU_PEAK_INST_S, "unit": "wave-instr/s",
+                "frac": None, "note": "no PMC summary for this configuration under profiles/"}
+    waves = 2 * ((n_env + 63) // 64)
+    inst = per * waves * chunk
+    achieved = inst / (kern_ms * 1e-3)
+    return {"bound": "valu-issue", "achieved": achieved, "peak": VALU_PEAK_INST_S, "unit": "wave-instr/s",
+            "frac": achieved / VALU_PEAK_INST_S, "valu_per_wave_step": per,
+            "one_wave_per_simd_ceiling_frac": 0.5,
+            "source": pmc.get("source")}
+
+
+def launch_plan(args, chunk):
+    """(timed steps, warm-up steps) in whole launches: >= min_launches timed, >= the requested
+    steps; warm-up >= min_warmup_launches and >= the requested warm-up."""
+    steps = max(args.min_launches * chunk, -(-args.steps // chunk) * chunk)
+    warm = max(args.min_warmup_launches * chunk, -(-args.warmup // chunk) * chunk)
+    return steps, warm
 
 
 def bench_rollout(args, rank, world, dev):
@@ -204,14 +309,18 @@ def bench_rollout(args, rank, world, dev):
     env.reset()
     env.init_step()
     chunk = args.chunk if args.mode == "rollout" else 1
-    steps = max(chunk, (args.steps // chunk) * chunk)
-    warm = max(chunk, (args.warmup // chunk) * chunk)
+    if args.mode == "step":
+        steps = max(args.min_launches, args.steps)
+        warm = max(args.min_warmup_launches, args.warmup)
+    else:
+        steps, warm = launch_plan(args, chunk)
     stream = torch.cuda.current_stream(dev)
-    # replay transitions of sampling events: written by the kernel with a device-side count and
-    # all-gathered over RCCL once per launch (no host synchronisation)
-    # capacity: measured steady-state rate 1 transition per ~390 env-steps (C3, K = 5000, launch 0:
-    # 1 per 369; tools/tcount.py), so 1 per 192 leaves 2x headroom (overflow is counted, not written)
-    tcap = max(1024, n_env * chunk // 192)
+    # replay transitions of sampling events, written by the kernel with a device-side count and
+    # gathered to the learner (rank 0) per launch.  Capacity per rank and launch: the measured
+    # steady-state rate is 1 transition per ~390 env-steps (C3; tools/tcount.py), so 1 per 192 is 2x
+    # headroom; floor n_env so the synchronised episode start (one event per env) always fits.
+    # Records beyond it are counted and reported ("dropped").
+    tcap = max(n_env, n_env * chunk // 192)
     gather = AsyncTransitionGather(tcap, 24, env.dtype, dev, world) if (world > 1 and not args.no_gather) else None
     out = {}
     launch_no = [0]
@@ -227,63 +336,78 @@ def bench_rollout(args, rank, world, dev):
                 torch.empty(n_env, dtype=torch.uint8, device=dev), torch.empty(n_env, dtype=torch.int32, device=dev),
                 torch.zeros(1, dtype=torch.int32, device=dev)]
 
-        def one():
+        def one(ev_pair=None):
+            if ev_pair:
+                ev_pair[0].record(stream)
             env._call("sit_step", act.data_ptr(), sac.data_ptr(), init.data_ptr(), *[b.data_ptr() for b in bufs],
                       env._stream())
+            if ev_pair:
+                ev_pair[1].record(stream)
     else:
         def one(ev_pair=None):
-            if gather:     # this launch's slot of the double-buffered transition gather
-                out["transitions"], out["transition_count"] = gather.buffers(launch_no[0])
+            i = launch_no[0]
+            if gather:     # this launch's slot of the pipelined transition gather
+                out["transitions"], out["transition_count"] = gather.buffers(i)
             if ev_pair:
                 ev_pair[0].record(stream)
             env.rollout(chunk, seed=args.seed, env_id_offset=offset, out=out,
                         transition_capacity=tcap if gather else 0)
             if ev_pair:
                 ev_pair[1].record(stream)
-            if gather:     # RCCL all-gather beside the next launch
-                gather.start(launch_no[0])
+            if gather:     # counts now, the valid records once this launch's counts are on the host
+                gather.start(i)
+                gather.progress(i - 1)
             launch_no[0] += 1
 
     for _ in range(warm // chunk):
         one()
     if gather:
         gather.finish()
+    gathered0, dropped0 = (gather.gathered, gather.dropped()) if gather else (0, 0)
     n_launch = steps // chunk
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
 
     def run():
         for i in range(n_launch):
-            if args.mode == "step":
-                ev[i][0].record(stream)
-                one()
-                ev[i][1].record(stream)
-            else:
-                one(ev[i])
+            one(ev[i])
         if gather:
             gather.finish()
     elapsed = timed(dev, world, run)
     launch_ms = [a.elapsed_time(b) for a, b in ev]
     if args.launch_trace:
         print("launch_ms " + " ".join(f"{x:.4f}" for x in launch_ms), file=sys.stderr)
-    kern_ms = float(np.mean(launch_ms))
+    kern_ms = float(np.median(launch_ms))
     st = env.get_state()
     rs = 4 if args.precision == 32 else 8
     alg = algorithmic_bytes_per_launch(n_env, chunk, rs, float(st["n_wpt"][1].double().mean().item()),
                                        float(st["n_wpt"][0].double().mean().item()), args.mode)
     env_steps = world * n_env * steps
-    rl = roofline(alg, kern_ms, latest_pmc(args.precision, args.mode, n_env, chunk))
+    pmc = latest_pmc(args.precision, args.mode, n_env, chunk)
+    rl = roofline(alg, kern_ms, pmc)
     rl["algorithmic_bytes_per_env_step"] = alg / (n_env * chunk)
     rl["launch_ms"] = stats_of(launch_ms)
+    rl["kernel_ms_statistic"] = "median over the timed launches (HIP events on the launch stream)"
     workload = ("C3: 65 536 ships = 32 768 two-ship envs per GPU, random IW actions, auto-reset" if world == 1 else
-                f"C4: {2 * n_env * world} ships sharded over {world} GPUs, random IW actions, RCCL transition gather")
-    return {
+                f"C4: {2 * n_env * world} ships sharded over {world} GPUs, random IW actions, RCCL gather of the "
+                f"replay transitions to the learner")
+    res = {
         "value": env_steps / elapsed, "steps": steps, "warmup": warm, "ms_per_step": elapsed * 1e3 / steps,
         "config": {"workload": workload, "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env,
-                   "fused_steps_per_launch": chunk, "mode": args.mode, "parallelism": f"env-shard x{world}",
-                   "ship_steps_per_s": 2 * env_steps / elapsed,
-                   "rccl_transition_gather": ("async, double-buffered, per launch" if gather is not None else None)},
+                   "fused_steps_per_launch": chunk, "n_launch": n_launch, "mode": args.mode,
+                   "parallelism": f"env-shard x{world}", "ship_steps_per_s": 2 * env_steps / elapsed,
+                   "steps_requested": args.steps, "warmup_requested": args.warmup},
         "roofline": rl,
+        "roofline_valu": roofline_valu(kern_ms, pmc, n_env, chunk) if args.mode == "rollout" else None,
     }
+    if gather is not None:
+        stats = torch.tensor([gather.gathered - gathered0, gather.dropped() - dropped0], dtype=torch.float64,
+                             device=dev)
+        res["config"]["rccl_transition_gather"] = {
+            "to": "rank 0 (learner)", "records_gathered": int(stats[0].item()),
+            "records_dropped": int(stats[1].item()), "capacity_per_rank_launch": tcap,
+            "bytes_per_record": 24 * rs, "pipelining": "count all-gather behind each launch; valid records "
+                                                       "point-to-point once the next launch is enqueued"}
+    return res
 
 
 def bench_policy(args, rank, world, dev):
@@ -368,13 +492,24 @@ def bench_policy(args, rank, world, dev):
 
 def main():
     args = parse()
-    rank, world, dev = setup_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args))
+    rank, world, dev = setup_dist(args)
+    if args.dry_run:
+        r = dry_run(args, rank, world, dev)
+        if rank == 0:
+            print(json.dumps(r), flush=True)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     r = bench_policy(args, rank, world, dev) if args.mode == "policy" else bench_rollout(args, rank, world, dev)
     result = {"metric": METRIC, "value": r["value"], "unit": "env-steps/s", "n_gpus": world, "steps": r["steps"],
               "warmup": r["warmup"], "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
               "vs_baseline": None, "dtype": "f32" if args.precision == 32 else "f64",
               "data": "synthetic (SURVEY §8(d) routes, island map of test_policy.py:189-194, Philox random IWs)",
               "config": r["config"], "roofline": r["roofline"]}
+    if r.get("roofline_valu"):
+        result["roofline_valu"] = r["roofline_valu"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.seed, args.cpu_baseline_workers)
     if rank == 0:

@@ -85,7 +85,9 @@ extern "C" {
 #define SIT_OBS_DIM 10 /* test n,e,psi,rpm,|e_ct|,P_me[kW], obs n,e,psi,|e_ct| */
 /* ---- replay transition record (memory.push, test_beds/main_ast.py:385-396) ----------
  *   [0:10] state (the observation before the step; reset()'s array at an episode start)
- *   [10] action (scoping angle a), [11] reward, [12:22] next_state,
+ *   [10] action: the SAC action of the event in [-1, 1] (the route angle a = action * pi/6; the
+ *        synthetic sampler's U[-1, 1] draw or the policy's squashed action; NaN in explicit mode),
+ *   [11] reward, [12:22] next_state,
  *   [22] mask (1 if the episode step reaches mask_horizon, else not done), [23] env id */
 #define SIT_TRANSITION_DIM 24
 /* Trajectory log rows per env and step (sit_rollout_args.log): ShipModelAST.store_simulation_data's
@@ -244,6 +246,12 @@ int sit_map_info(const sit_handle* h, int64_t* info, int32_t n);
  *   be NULL. */
 int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint8_t* inside,
                   uint8_t* hull, void* stream);
+/* Self-test of the IEEE float64 helpers the knife-edge decisions use (diagnostic; no reference
+ * counterpart): out[i] = op(a[i], b[i]) with op 0 a / b, 1 sqrt(a), 2 a*a + b*b, 3 (a + b) - a,
+ * 4 a*b + b*a, each correctly rounded per operation (numpy's float64).  fast_tu != 0 runs the copy
+ * compiled with the float32 step kernels' fast-math flags.  Device pointers. */
+int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, double* out, int32_t fast_tu,
+                     void* stream);
 /* Put every env into its construction-time state (as if freshly built).  Unlike
  * sit_reset this also re-initialises the shaft speed and all controller integrators. */
 int sit_restart(sit_handle* h, void* stream);

@@ -836,7 +836,9 @@ class OracleEnvs:
         sample = init | ((s["sampling_dist"] >= self.ab_len) & ~stopped)
         env_id = np.arange(self.n_env, dtype=np.uint64) + np.uint64(env_id_offset)
         u = sampler_uniform(seed, env_id, s["event"])
-        a = (u * 2.0 - 1.0) * (np.pi / 6.0)
+        act_n = u * 2.0 - 1.0                    # mode-0 action U[-1, 1] (uniform_policy.py:20-22)
+        a = act_n * (np.pi / 6.0)
+        self.last_action_n = np.where(sample, act_n, np.nan)   # the SAC action of the event
         iw_n = s["north"][1] + self.ab_len * np.cos(self.ab_alpha + a)
         iw_e = s["east"][1] + self.ab_len * np.sin(self.ab_alpha + a)
         s["iw_north"] = np.where(sample, iw_n, s["iw_north"])
@@ -845,7 +847,7 @@ class OracleEnvs:
         act = np.stack([s["iw_north"], s["iw_east"]], axis=1)
         return act, sample, init, np.where(sample, a, np.nan)
 
-    def policy_rollout(self, n_steps, seed, policy, env_id_offset=0):
+    def policy_rollout(self, n_steps, seed, policy, env_id_offset=0, mask_horizon=600):
         """The synchronous loop of test_beds/main_ast.py:310-412 with a policy choosing the IW
         (agent.select_action mode 1, :344-349): at every sampling event (episode start, or the
         sampling distance reaching AB_len while the obstacle ship runs) policy(state[m, 10],
@@ -855,23 +857,31 @@ class OracleEnvs:
         north, IW east, a, SAC_update) and the per-event policy actions."""
         s = self.s
         out = dict(next_state=[], reward=[], done=[], status=[], action=[])
+        trans = []
         env_id = np.arange(self.n_env, dtype=np.uint64) + np.uint64(env_id_offset)
         for _ in range(n_steps):
             init = s["ep_step"] == 0
             stopped = s["stop"][1].astype(bool)
             sample = init | ((s["sampling_dist"] >= self.ab_len) & ~stopped)
             ang = np.full(self.n_env, np.nan)
+            act_n = np.full(self.n_env, np.nan)
             idx = np.nonzero(sample)[0]
+            state_all = self.s["last_obs"].T.copy()
+            t_after = s["ep_step"] + 1
             if idx.size:
                 state = self.s["last_obs"].T[idx]
                 noise = sampler_normal(seed, env_id[idx], s["event"][idx])
                 a = np.asarray(policy(state, noise), dtype=np.float64).reshape(-1)
+                act_n[idx] = a
                 ang[idx] = a * (np.pi / 6.0)
                 s["iw_north"][idx] = s["north"][1][idx] + self.ab_len[idx] * np.cos(self.ab_alpha[idx] + ang[idx])
                 s["iw_east"][idx] = s["east"][1][idx] + self.ab_len[idx] * np.sin(self.ab_alpha[idx] + ang[idx])
                 s["event"][idx] = s["event"][idx] + 1
             act = np.stack([s["iw_north"], s["iw_east"]], axis=1)
             ns, rew, done, st = self.step(act, sample, init)
+            if idx.size:          # memory.push on sampling events (main_ast.py:385-396)
+                trans.append(self._transitions(idx, state_all, act_n, rew, ns, done, t_after, mask_horizon,
+                                               env_id_offset))
             out["next_state"].append(ns)
             out["reward"].append(rew)
             out["done"].append(done)
@@ -881,7 +891,18 @@ class OracleEnvs:
                 self.reset(done)
                 self.s["episodes"] = self.s["episodes"] + done.astype(np.int64)
                 self.init_step(done)
-        return {k: np.stack(v) for k, v in out.items()}
+        res = {k: np.stack(v) for k, v in out.items()}
+        res["transitions"] = np.concatenate(trans) if trans else np.zeros((0, 24))
+        return res
+
+    @staticmethod
+    def _transitions(idx, state, act_n, rew, ns, done, t_after, mask_horizon, env_id_offset):
+        """Replay records [state 10, action, reward, next_state 10, mask, env id] of the envs idx:
+        memory.push(state, action, reward, next_state, mask) with mask = 1 at the episode-length
+        horizon, else not done (test_beds/main_ast.py:385-396)."""
+        mask = np.where((mask_horizon > 0) & (t_after + 1 == mask_horizon), 1.0, 1.0 - done)
+        return np.concatenate([state[idx], act_n[idx, None], rew[idx, None], ns[idx], mask[idx, None],
+                               (idx + env_id_offset)[:, None].astype(np.float64)], axis=1)
 
     def rollout(self, n_steps, seed, auto_reset=True, env_id_offset=0, actions=None, mask_horizon=600):
         """K steps of the test_beds/main_ast.py:310-412 loop: reset+init_step on done, synthetic
@@ -893,6 +914,7 @@ class OracleEnvs:
         for k in range(n_steps):
             if actions is None:
                 act, sac, init, ang = self.sampler_actions(seed, env_id_offset)
+                act_n = self.last_action_n
             else:
                 act, sac, init = actions["action_ne"][k], actions["sac_update"][k], actions["init"][k]
                 ang = np.full(self.n_env, np.nan)
@@ -900,11 +922,8 @@ class OracleEnvs:
             t_after = self.s["ep_step"] + 1
             ns, rew, done, st = self.step(act, sac, init)
             if actions is None and np.any(sac):
-                idx = np.nonzero(sac)[0]
-                mask = np.where((mask_horizon > 0) & (t_after + 1 == mask_horizon), 1.0, 1.0 - done)
-                rec = np.concatenate([state[idx], ang[idx, None], rew[idx, None], ns[idx], mask[idx, None],
-                                      (idx + env_id_offset)[:, None].astype(np.float64)], axis=1)
-                trans.append(rec)
+                trans.append(self._transitions(np.nonzero(sac)[0], state, act_n, rew, ns, done, t_after,
+                                               mask_horizon, env_id_offset))
             out["next_state"].append(ns)
             out["reward"].append(rew)
             out["done"].append(done)

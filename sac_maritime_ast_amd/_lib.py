@@ -106,6 +106,7 @@ SIGNATURES = {
     "sit_policy_apply": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                                    c_void_p, c_void_p, c_void_p]),
     "sit_probe_map": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sit_selftest_f64": (c_int32, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "sit_restart": (c_int32, [c_void_p, c_void_p]),
     "sit_reset": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "sit_init_step": (c_int32, [c_void_p, c_void_p, c_void_p]),

@@ -11,9 +11,76 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sit.h"
 
 namespace sit {
+
+template <typename T>
+constexpr bool kIsF32 = std::is_same<T, float>::value;
+
+// --------------------------------------------------------------------------------------
+// IEEE float64 (round to nearest, no contraction, no reassociation) for knife-edge decisions.
+// The float32 step kernels are compiled with device fast-math (the TU keeps
+// -ffp-contract=fast-honor-pragmas so these scopes' contract(off) is honoured); add/sub/mul run in
+// pragma scopes, division and square root are the correctly rounded gfx950 sequences written
+// out with the div_scale/div_fmas/div_fixup and rsq builtins, which no fast-math flag rewrites.
+// Inputs converted from float32 are exact, so a decision taken here is the oracle's decision on
+// the same float32 state (checked bitwise against numpy: sit_selftest_f64, tests/test_gpu_parity.py).
+// --------------------------------------------------------------------------------------
+__device__ __forceinline__ double ieee_add(double a, double b) {
+#pragma clang fp reassociate(off) contract(off)
+  return a + b;
+}
+__device__ __forceinline__ double ieee_sub(double a, double b) {
+#pragma clang fp reassociate(off) contract(off)
+  return a - b;
+}
+__device__ __forceinline__ double ieee_mul(double a, double b) {
+#pragma clang fp reassociate(off) contract(off)
+  return a * b;
+}
+// a / b correctly rounded: the v_div_scale / v_rcp / Newton / v_div_fmas / v_div_fixup sequence
+__device__ __forceinline__ double ieee_div(double a, double b) {
+#pragma clang fp reassociate(off) contract(off)
+  bool f_den, f_num;
+  const double den = __builtin_amdgcn_div_scale(a, b, false, &f_den);
+  const double num = __builtin_amdgcn_div_scale(a, b, true, &f_num);
+  const double r0 = __builtin_amdgcn_rcp(den);
+  const double e0 = __builtin_fma(-den, r0, 1.0);
+  const double r1 = __builtin_fma(r0, e0, r0);
+  const double e1 = __builtin_fma(-den, r1, 1.0);
+  const double r2 = __builtin_fma(r1, e1, r1);
+  const double q = num * r2;
+  const double rem = __builtin_fma(-den, q, num);
+  (void)f_den;
+  return __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(rem, r2, q, f_num), b, a);
+}
+// sqrt(a) correctly rounded: rsq seed, Goldschmidt / Newton steps with fma, scaled for tiny a
+__device__ __forceinline__ double ieee_sqrt(double a) {
+#pragma clang fp reassociate(off) contract(off)
+  const bool tiny = a < 0x1.0p-767;
+  const double x = tiny ? __builtin_amdgcn_ldexp(a, 256) : a;
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  g = tiny ? __builtin_amdgcn_ldexp(g, -128) : g;
+  // +-0, +inf and NaN pass through unchanged (class mask: NaNs, -0, +0, +inf)
+  return __builtin_amdgcn_class(x, 0x263) ? a : g;
+}
+// a^2 + b^2 as numpy evaluates (dn ** 2 + de ** 2): two roundings of the squares, one of the sum
+__device__ __forceinline__ double ieee_sq2(double a, double b) { return ieee_add(ieee_mul(a, a), ieee_mul(b, b)); }
+// x * y + z * w as numpy evaluates it (no fused multiply-add)
+__device__ __forceinline__ double ieee_dot2(double x, double y, double z, double w) {
+  return ieee_add(ieee_mul(x, y), ieee_mul(z, w));
+}
 
 constexpr int kWave = 64;         // CDNA wavefront
 #ifndef SIT_ENVS_PER_BLOCK
@@ -85,6 +152,14 @@ struct Consts {
   T fx0, fy0, finvx, finvy;   // fine class grid origin and 1 / cell size
   // trajectory log only (store_simulation_data, fuel model)
   T el_cap, fuel_me_a, fuel_me_b, fuel_me_c, fuel_dg_a, fuel_dg_b, fuel_dg_c, rad2deg;
+  // the float64 values of every threshold and of the gains a knife-edge re-evaluation needs
+  // (float32 handle: decisions whose float32 margin lies inside the float32 error band are
+  // re-taken in float64 from the float32 state; float64 handle: the decisions themselves)
+  struct X64 {
+    double los_r, windup, e_tol, arrival, rpm_max, min_dist, blackout;
+    double dt, kp1, ki1, kp2, ki2, avail_prop, me_cap, hotel, load_el_gen, bias_scale, bias_max;
+    double half_len, theta;
+  } x;
 };
 
 // island map (obstacle.py:92-124): edge i of the closed rings runs from (ax, ay) to (bx, by);
@@ -297,25 +372,56 @@ struct Ship {
 
 // rudder_angle_from_sampled_route + throttle (controllers.py:306-314, 138-143, 52-62, 81-93,
 // 180-189; LOS_guidance.py:88-121).  Returns rudder, throttle and |e_ct|.
+// LOS_guidance.py:110-120 in the reference's float64 arithmetic from the (float32) state: the
+// cross-track error |e|, the (clamped) e / Delta and whether the integrator accepts it
+template <typename T>
+__device__ __forceinline__ void los_exact(const Consts<T>& c, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
+                                                    double& ect_abs, double& q, double& sum, bool& accept) {
+  const double dx = ieee_sub(cn, pn), dy = ieee_sub(ce, pe);
+  const double len = ieee_sqrt(ieee_sq2(dx, dy));
+  const double sa = len > 0.0 ? ieee_div(dy, len) : 0.0, ca = len > 0.0 ? ieee_div(dx, len) : 1.0;
+  double ect = ieee_add(ieee_mul(-ieee_sub(n, pn), sa), ieee_mul(ieee_sub(e, pe), ca));
+  ect_abs = fabs(ect);
+  const double r2 = ieee_mul(c.x.los_r, c.x.los_r);
+  if (ieee_mul(ect, ect) >= r2) ect = ieee_mul(0.99, c.x.los_r);
+  q = ieee_div(ect, ieee_sqrt(ieee_sub(r2, ieee_mul(ect, ect))));
+  sum = ieee_add((double)ect_int, q);
+  accept = fabs(sum) <= c.x.windup;
+}
+
 template <typename T>
 __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s, Route<T>& rt,
-                                                 T v_des, T& rudder, T& thr, T& ect_abs, T& psi_ref_out) {
-  // next_wpt: acceptance test evaluated in double, without contraction, from the stored
-  // values (bit-identical to the float64 reference for identical inputs)
-  {
-    const double dn = (double)rt.cn - (double)s.n;
-    const double de = (double)rt.ce - (double)s.e;
-    const double d2 = __dadd_rn(__dmul_rn(dn, dn), __dmul_rn(de, de));
-    rt.advance(d2 <= c.ra2 && rt.nw > s.k + 1, s.k);
-  }
+                                                 T v_des, T& rudder, T& thr, T& ect_abs, T& psi_ref_out,
+                                                 double& ect_x) {
+  // next_wpt: acceptance test evaluated in IEEE float64 from the stored values (the reference's
+  // decision for the same state; LOS_guidance.py:96)
+  rt.advance(ieee_sq2(ieee_sub(rt.cn, s.n), ieee_sub(rt.ce, s.e)) <= c.ra2 && rt.nw > s.k + 1, s.k);
   const T pn = rt.pn, pe = rt.pe;
   const T alpha = rt.alpha, sa = rt.sa, ca = rt.ca;
   T ect = -(s.n - pn) * sa + (s.e - pe) * ca;
   ect_abs = xabs(ect);
-  if (ect * ect >= c.los_r2) ect = c.los_clamp;           // sign lost (Q5)
+  ect_x = (double)ect_abs;
+  bool clamp = ect * ect >= c.los_r2;
+  if (clamp) ect = c.los_clamp;                           // sign lost (Q5)
   const T delta = xsqrt(c.los_r2 - ect * ect);
-  const T q = ect / delta;
-  if (xabs(s.ect_int + q) <= c.windup) s.ect_int += q;
+  T q = ect / delta;
+  T sum = s.ect_int + q;
+  bool accept = xabs(sum) <= c.windup;
+  if constexpr (kIsF32<T>) {
+    // knife edges of the clamp (|e| = lookahead), of the navigation-failure threshold (|e| =
+    // e_tolerance) and of the anti-windup limit: float32 carries ~1e-3 m of rounding in e and
+    // ~3e-4 in the integral, so inside these bands the decisions are re-taken in float64
+    const bool knife = xmin(xabs(ect_abs - c.los_r), xabs(ect_abs - c.e_tol)) < T(0.05) ||
+                       xabs(xabs(sum) - c.windup) < T(0.02);
+    if (knife) {
+      double qd, sd;
+      los_exact(c, s.n, s.e, pn, pe, rt.cn, rt.ce, s.ect_int, ect_x, qd, sd, accept);
+      ect_abs = (T)ect_x;
+      q = (T)qd;
+      sum = (T)sd;
+    }
+  }
+  if (accept) s.ect_int = sum;
   const T chi = xatan(-q - s.ect_int * c.los_ki);
   const T psi_ref = alpha + chi;
   psi_ref_out = psi_ref;
@@ -333,6 +439,63 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
   const T e2 = wdes - s.u;
   s.i2 = s.i2 + e2 * c.dt;
   thr = e2 * c.kp2 + s.i2 * c.ki2;
+}
+
+// EngineThrottleFromSpeedSetPoint.throttle (controllers.py:52-62, 138-143) in the reference's
+// float64 arithmetic from the pre-step integrals i1, i2 and surge u; with the collision bias of
+// MSRL_Env.py:244-251 when `bias`
+template <typename T>
+__device__ __forceinline__ double throttle_exact(const Consts<T>& c, T u, T v_des, T i1, T i2, bool bias) {
+  const double e1 = ieee_sub(v_des, u);
+  const double ii1 = ieee_add(i1, ieee_mul(e1, c.x.dt));
+  const double wdes = ieee_dot2(e1, c.x.kp1, ii1, c.x.ki1);
+  const double e2 = ieee_sub(wdes, u);
+  const double ii2 = ieee_add(i2, ieee_mul(e2, c.x.dt));
+  double thr = ieee_dot2(e2, c.x.kp2, ii2, c.x.ki2);
+  if (bias) thr = fmax(0.0, fmin(ieee_mul(thr, c.x.bias_scale), c.x.bias_max));
+  return thr;
+}
+
+// distribute_load(...).load_on_main_engine / 1000 in float64 (ship_engine.py:46-76)
+template <typename T>
+__device__ __forceinline__ double power_me_kw_exact(const Consts<T>& c, double thr) {
+  const double total = ieee_mul(thr, c.x.avail_prop);
+  double load_me;
+  if (c.sg_mode == 0) load_me = fmin(total, c.x.me_cap);
+  else if (c.sg_mode == 1) load_me = ieee_sub(ieee_add(total, c.x.hotel), c.x.load_el_gen);
+  else load_me = total;
+  return ieee_div(load_me, 1000.0);
+}
+
+// is_mechanical_failure (MSRL_env_ex.py:554-558): |shaft speed * 30 / pi| > shaft_rpm_max, with
+// rpm = w * 30 / pi (ship_model.py:652) re-taken in float64 near the threshold
+template <typename T>
+__device__ __forceinline__ bool rpm_fails(const Consts<T>& c, T w, T rpm) {
+  if constexpr (kIsF32<T>) {
+    if (xabs(xabs(rpm) - c.rpm_max) < T(0.01)) return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > c.x.rpm_max;
+    return xabs(rpm) > c.rpm_max;
+  } else {
+    return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > c.x.rpm_max;
+  }
+}
+
+// sqrt(dn^2 + de^2) <= r (arrival, MSRL_env_ex.py:754, 829) / dn^2 + de^2 < r^2 (collision, :592)
+// as the reference evaluates them in float64, decided in float32 away from the boundary
+template <typename T>
+__device__ __forceinline__ bool within_radius(T n0, T e0, T n1, T e1, T r, double r_x) {
+  if constexpr (kIsF32<T>) {
+    const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de, r2 = r * r;
+    if (xabs(d2 - r2) > T(1e-4) * r2) return d2 <= r2;
+  }
+  return ieee_sqrt(ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1))) <= r_x;
+}
+template <typename T>
+__device__ __forceinline__ bool closer_than(T n0, T e0, T n1, T e1, T r2, double r_x) {
+  if constexpr (kIsF32<T>) {
+    const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de;
+    if (xabs(d2 - r2) > T(1e-4) * r2) return d2 < r2;
+  }
+  return ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1)) < ieee_mul(r_x, r_x);
 }
 
 // One row of ShipModelAST.store_simulation_data (ship_model.py:645-684) from the pre-integration
@@ -444,6 +607,7 @@ __device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T 
 // only runs when the orientation filter is uncertain
 template <typename T>
 __device__ __attribute__((noinline)) int exact_sign_diff(T a, T b, T c, T d) {
+#pragma clang fp reassociate(off) contract(off)
   const T p1 = a * b, e1 = xfma(a, b, -p1);
   const T p2 = c * d, e2 = xfma(c, d, -p2);
   auto two_sum = [](T x, T y, T& err) { const T s = x + y; const T bb = s - x; err = (x - (s - bb)) + (y - bb); return s; };
@@ -466,7 +630,7 @@ __device__ __attribute__((noinline)) int exact_sign_diff(T a, T b, T c, T d) {
 // GEOS CGAlgorithmsDD::orientationIndex(p1, p2, q): orientationIndexFilter, exact fallback
 template <typename T>
 __device__ __forceinline__ int orientation(T p1x, T p1y, T p2x, T p2y, T qx, T qy) {
-#pragma clang fp contract(off)
+#pragma clang fp reassociate(off) contract(off)
   const T ax = p1x - qx, by = p2y - qy, ay = p1y - qy, bx = p2x - qx;
   const T dl = ax * by;
   const T dr = ay * bx;
@@ -477,10 +641,14 @@ __device__ __forceinline__ int orientation(T p1x, T p1y, T p2x, T p2y, T qx, T q
 }
 
 // GEOS RayCrossingCounter::countSegment for one segment (x = east, y = north), written with
-// predication: the only branch left is the rare exact-orientation fallback.
-template <typename T>
-__device__ __forceinline__ void count_segment(T p1x, T p1y, T p2x, T p2y, T qx, T qy, uint32_t bit,
-                                              uint32_t& parity, uint32_t& onb) {
+// predication: the only branch left is the rare exact-orientation fallback.  Always evaluated in
+// float64 (the reference's arithmetic): edge vertices (float32 in the float32 handle, exact for
+// the reference's integer map) are promoted, and the query point is the caller's exact float64
+// point (a hull corner n +- l/2 of a float32 position is exact in float64, not in float32), so the
+// float32 handle decides containment exactly as the reference does for the same point.
+__device__ __forceinline__ void count_segment(double p1x, double p1y, double p2x, double p2y, double qx, double qy,
+                                              uint32_t bit, uint32_t& parity, uint32_t& onb) {
+#pragma clang fp reassociate(off) contract(off)
   // GEOS order: strictly-left segments and the end vertex are resolved first, horizontal
   // segments never count, straddling segments count when the point is to their left
   if (p1x < qx && p2x < qx) return;
@@ -498,10 +666,11 @@ __device__ __forceinline__ void count_segment(T p1x, T p1y, T p2x, T p2y, T qx, 
   parity ^= (live & (oo > 0)) ? bit : 0u;
 }
 
-// Polygon.contains(Point(e, n)) for any polygon by a full scan (fallback path)
+// Polygon.contains(Point(e, n)) for any polygon by a full scan (fallback path); (qn, qe) is the
+// exact float64 query point
 template <typename T>
-__device__ bool point_in_polys(const Map<T>& m, T n, T e) {
-  const T qx = e, qy = n;
+__device__ bool point_in_polys(const Map<T>& m, double qn, double qe) {
+  const double qx = qe, qy = qn;
   uint32_t par = 0, onb = 0;
   for (int p = 0; p < m.n_poly; ++p) {
     const T* bb = m.bbox + 4 * p;
@@ -565,11 +734,12 @@ __device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   return xsqrt(best);
 }
 
-// Polygon.contains for two points sharing y (= n): bit 0 / bit 1 for x0 / x1
+// Polygon.contains for two points sharing y (= n): bit 0 / bit 1 for x0 / x1 (exact float64
+// query coordinates; the band index in T, its lists carry a 1 m margin)
 template <typename T>
-__device__ int pip_pair_indexed(const Consts<T>& c, const Map<T>& m, T n, T x0, T x1) {
+__device__ int pip_pair_indexed(const Consts<T>& c, const Map<T>& m, double n, double x0, double x1) {
   if (!m.use_index) return (int)point_in_polys(m, n, x0) | ((int)point_in_polys(m, n, x1) << 1);
-  const T fb = (n - c.by0) * c.binv;
+  const T fb = ((T)n - c.by0) * c.binv;
   if (!(fb >= T(0) && fb < T(kBands))) return 0;   // beyond every edge's y-range
   const int b = (int)fb;
   uint32_t par0 = 0, onb0 = 0, par1 = 0, onb1 = 0;
@@ -585,9 +755,9 @@ __device__ int pip_pair_indexed(const Consts<T>& c, const Map<T>& m, T n, T x0, 
 }
 
 template <typename T>
-__device__ bool pip_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
+__device__ bool pip_indexed(const Consts<T>& c, const Map<T>& m, double n, double e) {
   if (!m.use_index) return point_in_polys(m, n, e);
-  const T fb = (n - c.by0) * c.binv;
+  const T fb = ((T)n - c.by0) * c.binv;
   if (!(fb >= T(0) && fb < T(kBands))) return false;
   const int b = (int)fb;
   uint32_t par = 0, onb = 0;
@@ -622,9 +792,10 @@ __device__ __forceinline__ int fine_class(const Consts<T>& c, const Map<T>& m, T
 }
 
 // Polygon.contains(Point(e, n)) for a point in mixed class cell `cell` (class word `word`):
-// the cell's constant crossing parity plus GEOS's count over the cell's live edges only
+// the cell's constant crossing parity plus GEOS's count over the cell's live edges only, at the
+// exact float64 point (n, e)
 template <typename T>
-__device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t word, T n, T e) {
+__device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t word, double n, double e) {
   const uint32_t mixed = (word >> 1) & 0x55555555u;
   const int r = m.frank[cell >> 4] + __popc(mixed & ((1u << ((cell & 15) * 2)) - 1u));
   const uint2 rec = m.crec[r];
@@ -638,8 +809,9 @@ __device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t wor
   return (par & ~onb) != 0;
 }
 
-// Polygon.contains(Point(e, n)): fine-grid class when the cell is pure; the mixed cell's
-// record (or, without records, a band scan) otherwise
+// Polygon.contains(Point(e, n)): fine-grid class when the cell is pure (a pure cell has no
+// boundary within 1 m, far beyond float32 rounding of the cell index); the mixed cell's record
+// (or, without records, a band scan) in float64 otherwise
 template <typename T>
 __device__ bool pip_point(const Consts<T>& c, const Map<T>& m, T n, T e) {
   int cell;
@@ -679,8 +851,11 @@ __device__ __forceinline__ bool hull_in_terrain_cls(const Consts<T>& c, const Ma
 template <typename T>
 __device__ bool hull_corners(const Consts<T>& c, const Map<T>& m, T n, T e) {
   const T h = c.half_len;
-  // near shore: each corner by its fine-grid class; a corner in a mixed cell by the cell's
-  // record (or a band scan without records)
+  // the corners as the reference forms them (n +- l/2 in float64; exact for a float32 position)
+  const double hx = c.x.half_len;
+  const double nlo = ieee_sub(n, hx), nhi = ieee_add(n, hx), elo = ieee_sub(e, hx), ehi = ieee_add(e, hx);
+  // near shore: each corner by its fine-grid class (cell index in T: pure cells have a 1 m margin);
+  // a corner in a mixed cell by the cell's record (or a band scan without records)
   if (m.use_cells) {
     int l00, l01, l10, l11;
     uint32_t w00, w01, w10, w11;
@@ -688,18 +863,18 @@ __device__ bool hull_corners(const Consts<T>& c, const Map<T>& m, T n, T e) {
     const int c10 = fine_lookup(c, m, n + h, e - h, l10, w10), c11 = fine_lookup(c, m, n + h, e + h, l11, w11);
     if (c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1) return true;
     bool hit = false;
-    if (c00 == 2) hit |= pip_cell(m, l00, w00, n - h, e - h);
-    if (c01 == 2) hit |= pip_cell(m, l01, w01, n - h, e + h);
-    if (c10 == 2) hit |= pip_cell(m, l10, w10, n + h, e - h);
-    if (c11 == 2) hit |= pip_cell(m, l11, w11, n + h, e + h);
+    if (c00 == 2) hit |= pip_cell(m, l00, w00, nlo, elo);
+    if (c01 == 2) hit |= pip_cell(m, l01, w01, nlo, ehi);
+    if (c10 == 2) hit |= pip_cell(m, l10, w10, nhi, elo);
+    if (c11 == 2) hit |= pip_cell(m, l11, w11, nhi, ehi);
     return hit;
   }
   const int c00 = fine_class(c, m, n - h, e - h), c01 = fine_class(c, m, n - h, e + h);
   const int c10 = fine_class(c, m, n + h, e - h), c11 = fine_class(c, m, n + h, e + h);
   if (c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1) return true;
   bool hit = false;
-  if (c00 >= 2 || c01 >= 2) hit |= pip_pair_indexed(c, m, n - h, e - h, e + h) != 0;
-  if (c10 >= 2 || c11 >= 2) hit |= pip_pair_indexed(c, m, n + h, e - h, e + h) != 0;
+  if (c00 >= 2 || c01 >= 2) hit |= pip_pair_indexed(c, m, nlo, elo, ehi) != 0;
+  if (c10 >= 2 || c11 >= 2) hit |= pip_pair_indexed(c, m, nhi, elo, ehi) != 0;
   return hit;
 }
 

@@ -225,8 +225,9 @@ __device__ __forceinline__ void reset_ship(const Scen<T>& sc, int type, int env,
 template <typename T>
 __device__ __forceinline__ void init_step_ship(const Consts<T>& c, Ship<T>& s, Route<T>& rt, T v_des) {
   T rudder, thr, ect, sp, cp, psi_ref;
+  double ect_x;
   xsincos(s.psi, &sp, &cp);
-  guidance_control(c, s, rt, v_des, rudder, thr, ect, psi_ref);
+  guidance_control(c, s, rt, v_des, rudder, thr, ect, psi_ref, ect_x);
   ship_dynamics(c, s, thr, rudder, sp, cp);
   rt.fixup(s.k);
 }
@@ -505,7 +506,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #endif
     bool sac = false, init_f = false;
     double ang = 0.0;                  // the sampled angle; has_ang: drawn on device this step
+    double act_n = 0.0;                // the SAC action of the event: ang / (pi / 6), in [-1, 1]
     bool has_ang = false;
+    double ect_x = 0.0;                // |e_ct| for the navigation-failure decision (exact, see guidance_control)
+    bool mech = false, blk = false;    // test ship: mechanical / blackout failure (decided pre-integration)
     bool stall_now = false;
     if (MODE == kPolicy && act && !stalled && need && !ready) {
       // sampling event without an action: wait for the policy; the obstacle lane queues the
@@ -533,6 +537,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           init_f = (ep_step == 0);
           sac = need;
           if (sac) {                     // the policy's squashed action scales the route angle
+            act_n = (double)pa;
             ang = (double)pa * (M_PI / 6.0);
             has_ang = true;
             iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
@@ -541,9 +546,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         } else if (MODE == kSynth) {
           init_f = (ep_step == 0);
           sac = init_f || ((double)samp >= ab_len && !s.stop);
-          if (sac) {
+          if (sac) {                     // mode-0 action U[-1, 1] (uniform_policy.py:20-22) scaled by pi/6
             const double u01 = sampler_uniform(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
-            ang = (u01 * 2.0 - 1.0) * (M_PI / 6.0);
+            act_n = u01 * 2.0 - 1.0;
+            ang = act_n * (M_PI / 6.0);
             has_ang = true;
             iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
             ++event;
@@ -562,6 +568,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           }
           s.ticks += 2;                  // stop path: next_time() twice, no integration (Q10)
           o_rpm = s.lrpm; o_ect = s.lect; o_pme = s.lpme;
+          ect_x = (double)o_ect;
         } else {
           if (sac) {                     // update_route: insert at index -1 (Q16)
             if (!rt.insert(iwn, iwe, s.k, a.cap)) bits |= SIT_ST_ROUTE_OVERFLOW;
@@ -569,7 +576,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           }
           const T pre_n = s.n, pre_e = s.e;
           T rudder, thr, psi_ref;
-          guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref);
+          guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_x);
           o_rpm = s.w * c.rpm_k;
           o_pme = power_me_kw(c, thr);
           s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
@@ -590,13 +597,20 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       } else {
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
-        guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref);
+        const T i1_0 = s.i1, i2_0 = s.i2;   // pre-step integrals (blackout knife edge)
+        guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_x);
         if (c.collision_bias) {          // is_collision_imminent() on all-zero states (Q1)
           thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
           rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
         }
         o_rpm = s.w * c.rpm_k;
         o_pme = power_me_kw(c, thr);
+        // failure predicates on pre-integration values (MSRL_env_ex.py:554-558, 578-582), exact:
+        // float64 where the float32 margin is inside the float32 band (always for the float64 handle)
+        mech = rpm_fails(c, s.w, o_rpm);
+        blk = o_pme > c.blackout_kw;
+        if (!kIsF32<T> || xabs(o_pme - c.blackout_kw) <= T(1e-4) * (xabs(o_pme) + T(1)))
+          blk = power_me_kw_exact(c, throttle_exact(c, s.u, v_des, i1_0, i2_0, c.collision_bias != 0)) > c.x.blackout;
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
         if (p_lg) store_log_row(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
         ship_dynamics(c, s, thr, rudder, sp, cp);
@@ -623,8 +637,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #ifdef SIT_DIAG_PATHS
       diag_lane(c, map, s.n, s.e, dobst, type == 1, iwn, iwe, dv);
 #endif
-      const T dn_end = s.n - rt.end_n, de_end = s.e - rt.end_e;
-      const bool arrive = xsqrt(dn_end * dn_end + de_end * de_end) <= c.arrival_radius;
+      const bool arrive = within_radius(s.n, s.e, rt.end_n, rt.end_e, c.arrival_radius, c.x.arrival);
       const bool horizon = outside(c, s.n, s.e, c.half_len);
       int stop = s.stop;
       bool done = false;
@@ -636,8 +649,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           t[row_step] = (T(1) - dobst / c.max_n) / T(100);
           t[2 * row_step] = r_nt;
         }
-        const bool pred[6] = {arrive, horizon, terrain, xabs(o_rpm) > c.rpm_max, xabs(o_ect) > c.e_tol,
-                              o_pme > c.blackout_kw};
+        const bool pred[6] = {arrive, horizon, terrain, mech, ect_x > c.x.e_tol, blk};
         const T rew[6] = {T(0), T(0), T(1000), T(1000), T(1000), T(1000)};
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -679,7 +691,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           stop = 1; done = true;
           bits |= SIT_ST_OBS_IW_TERMINAL;
         }
-        if (xabs(o_ect) > c.e_tol || (double)samp > ab_len * (double)c.theta) {
+        if (ect_x > c.x.e_tol || (double)samp > ieee_mul(ab_len, c.x.theta)) {
           if (!stop) r_term = r_term - T(1000);
           stop = 1; done = true;
           bits |= SIT_ST_OBS_NAVIGATION;
@@ -717,7 +729,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     }
     if (live) {
       const T dn = x.n[0][lane] - x.n[1][lane], de = x.e[0][lane] - x.e[1][lane];
-      const bool coll = dn * dn + de * de < c.min_dist2;
+      const bool coll = closer_than(x.n[0][lane], x.e[0][lane], x.n[1][lane], x.e[1][lane], c.min_dist2, c.x.min_dist);
       const uint32_t bt = x.bits[0][lane], bo = x.bits[1][lane];
       env_done = ((bt | bo) & kDoneBit) || coll;
       if (coll) s.stop = 1;
@@ -757,9 +769,10 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         if (slot >= 0 && slot < a.io.transition_capacity) {
           T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
           for (int j = 0; j < 4; ++j) rec[6 + j] = lo[j];
-          rec[10] = angle_or_nan(has_ang, (T)ang);
+          // the SAC action of the event in [-1, 1] (memory.push(state, action, ...), main_ast.py:395):
+          // the sampler's U[-1, 1] draw or the policy's squashed action; NaN without a device draw
+          rec[10] = angle_or_nan(has_ang, (T)act_n);
           rec[18] = s.n; rec[19] = s.e; rec[20] = s.psi; rec[21] = o_ect;
-          if (MODE == kPolicy) rec[10] = pa;   // the policy's action (memory.push, main_ast.py:395)
           rec[23] = (T)(a.io.env_id_offset + env);
         }
       }
@@ -925,6 +938,23 @@ __global__ __launch_bounds__(256) void k_probe_map(const KArgs<T> a, int n, cons
   if (dist) dist[i] = d;
   if (inside) inside[i] = pip_point(a.c, a.map, pn, pe) ? 1 : 0;
   if (hull) hull[i] = hull_in_terrain(a.c, a.map, pn, pe, d) ? 1 : 0;
+}
+
+// the IEEE float64 helpers of the knife-edge decisions (sit_selftest_f64, one thread per input):
+// compiled into both translation units, so the fast-math one is checked bitwise against numpy
+__global__ __launch_bounds__(256) void k_selftest_f64(int op, int n, const double* a, const double* b, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double x = a[i], y = b[i];
+  double r;
+  switch (op) {
+    case 0: r = ieee_div(x, y); break;
+    case 1: r = ieee_sqrt(x); break;
+    case 2: r = ieee_sq2(x, y); break;
+    case 3: r = ieee_sub(ieee_add(x, y), x); break;
+    default: r = ieee_dot2(x, y, y, x); break;
+  }
+  out[i] = r;
 }
 
 // policy head + scatter (sit_policy_apply, one thread per request row): the squashed Gaussian
@@ -1125,6 +1155,21 @@ Consts<T> make_consts(const sit_handle* h) {
   c.fuel_me_a = (T)p.fuel_me_a; c.fuel_me_b = (T)p.fuel_me_b; c.fuel_me_c = (T)p.fuel_me_c;
   c.fuel_dg_a = (T)p.fuel_dg_a; c.fuel_dg_b = (T)p.fuel_dg_b; c.fuel_dg_c = (T)p.fuel_dg_c;
   c.rad2deg = (T)(180.0 / M_PI);
+  // float64 thresholds and gains (knife-edge decisions; MSRL_env_ex.py:119, 554-603, 754, 829)
+  c.x.los_r = p.lookahead_distance;
+  c.x.windup = p.integrator_windup_limit;
+  c.x.e_tol = p.e_tolerance;
+  c.x.arrival = p.arrival_radius;
+  c.x.rpm_max = p.shaft_rpm_max;
+  c.x.min_dist = p.minimum_ship_distance;
+  c.x.blackout = me / 1000;
+  c.x.dt = p.integration_step;
+  c.x.kp1 = p.kp_ship_speed; c.x.ki1 = p.ki_ship_speed;
+  c.x.kp2 = p.kp_shaft_speed; c.x.ki2 = p.ki_shaft_speed;
+  c.x.avail_prop = avail; c.x.me_cap = me; c.x.hotel = hotel; c.x.load_el_gen = std::min(hotel, el);
+  c.x.bias_scale = p.bias_throttle_scale; c.x.bias_max = p.bias_throttle_max;
+  c.x.half_len = l / 2;
+  c.x.theta = p.theta;
   return c;
 }
 
@@ -1216,6 +1261,22 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   if (rc) return rc;
   HIP_TRY(h, hipGetLastError());
   return SIT_OK;
+}
+
+template <typename T>
+int launch_probe(sit_handle* h, int n, const void* pts_ne, void* dist, uint8_t* inside, uint8_t* hull,
+                 hipStream_t stream) {
+  const KArgs<T> a = make_args<T>(h);
+  const int blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(k_probe_map<T>, dim3(blocks), dim3(256), 0, stream, a, n, (const T*)pts_ne, (T*)dist,
+                     inside, hull);
+  HIP_TRY(h, hipGetLastError());
+  return SIT_OK;
+}
+
+int launch_selftest(int op, int n, const double* a, const double* b, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(k_selftest_f64, dim3((n + 255) / 256), dim3(256), 0, stream, op, n, a, b, out);
+  return hipGetLastError() == hipSuccess ? SIT_OK : SIT_E_HIP;
 }
 
 }  // namespace

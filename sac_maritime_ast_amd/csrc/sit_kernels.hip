@@ -8,13 +8,28 @@ namespace {
 #ifdef SIT_SPLIT_F32
 }  // namespace
 int sit_launch_steps_f32(sit_handle* h, const void* io, void* stream);   // sit_steps_f32.hip
+int sit_launch_probe_f32(sit_handle* h, int n, const void* pts_ne, void* dist, uint8_t* inside, uint8_t* hull,
+                         void* stream);
+int sit_launch_selftest_f32tu(int op, int n, const double* a, const double* b, double* out, void* stream);
 namespace {
 int launch_steps_f32(sit_handle* h, const StepIO<float>& io, void* stream) {
   return sit_launch_steps_f32(h, &io, stream);
 }
+int launch_probe_f32(sit_handle* h, int n, const void* pts, void* dist, uint8_t* inside, uint8_t* hull, void* stream) {
+  return sit_launch_probe_f32(h, n, pts, dist, inside, hull, stream);
+}
+int launch_selftest_f32tu(int op, int n, const double* a, const double* b, double* out, void* stream) {
+  return sit_launch_selftest_f32tu(op, n, a, b, out, stream);
+}
 #else   // single-TU build (diagnostic builds): float32 step kernels compiled here, strict fp
 int launch_steps_f32(sit_handle* h, const StepIO<float>& io, void* stream) {
   return launch_steps<float>(h, io, (hipStream_t)stream);
+}
+int launch_probe_f32(sit_handle* h, int n, const void* pts, void* dist, uint8_t* inside, uint8_t* hull, void* stream) {
+  return launch_probe<float>(h, n, pts, dist, inside, hull, (hipStream_t)stream);
+}
+int launch_selftest_f32tu(int op, int n, const double* a, const double* b, double* out, void* stream) {
+  return launch_selftest(op, n, a, b, out, (hipStream_t)stream);
 }
 #endif
 
@@ -52,18 +67,16 @@ int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint
   if (!h->have_map) return fail(h, SIT_E_STATE, "sit_load_map has not been called");
   if (n < 0 || (n > 0 && !pts_ne)) return fail(h, SIT_E_INVALID, "need n >= 0 points");
   if (n == 0) return SIT_OK;
-  const int blocks = (n + 255) / 256;
-  if (h->precision == SIT_F64) {
-    const KArgs<double> a = make_args<double>(h);
-    hipLaunchKernelGGL(k_probe_map<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, n,
-                       (const double*)pts_ne, (double*)dist, inside, hull);
-  } else {
-    const KArgs<float> a = make_args<float>(h);
-    hipLaunchKernelGGL(k_probe_map<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, n,
-                       (const float*)pts_ne, (float*)dist, inside, hull);
-  }
-  HIP_TRY(h, hipGetLastError());
-  return SIT_OK;
+  if (h->precision == SIT_F64) return launch_probe<double>(h, n, pts_ne, dist, inside, hull, (hipStream_t)stream);
+  return launch_probe_f32(h, n, pts_ne, dist, inside, hull, stream);
+}
+
+int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, double* out, int32_t fast_tu,
+                     void* stream) {
+  if (op < 0 || op > 4 || n < 0 || (n > 0 && (!a || !b || !out))) return SIT_E_INVALID;
+  if (n == 0) return SIT_OK;
+  return fast_tu ? launch_selftest_f32tu(op, n, a, b, out, stream)
+                 : launch_selftest(op, n, a, b, out, (hipStream_t)stream);
 }
 
 int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t head_stride, const void* noise,

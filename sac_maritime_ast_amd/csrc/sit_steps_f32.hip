@@ -9,3 +9,15 @@
 int sit_launch_steps_f32(sit_handle* h, const void* io, void* stream) {
   return launch_steps<float>(h, *static_cast<const StepIO<float>*>(io), (hipStream_t)stream);
 }
+
+// the float32 map predicates of the step kernels (sit_probe_map on a float32 handle): same TU and
+// flags as the step kernels, so the probes check the code the benchmark runs
+int sit_launch_probe_f32(sit_handle* h, int n, const void* pts_ne, void* dist, uint8_t* inside, uint8_t* hull,
+                         void* stream) {
+  return launch_probe<float>(h, n, pts_ne, dist, inside, hull, (hipStream_t)stream);
+}
+
+// the IEEE float64 helpers as compiled under this TU's fast-math flags (sit_selftest_f64)
+int sit_launch_selftest_f32tu(int op, int n, const double* a, const double* b, double* out, void* stream) {
+  return launch_selftest(op, n, a, b, out, (hipStream_t)stream);
+}

@@ -1,5 +1,6 @@
-"""N > 1 path on CPU (gloo, world size 2): env sharding by global env id plus the transition
-all-gather of sac_maritime_ast_amd.shard.  The CPU oracle stands in for the GPU env here; the
+"""N > 1 path on CPU (gloo, world size 2): env sharding by global env id plus the gather of the
+replay transitions to the learner (sac_maritime_ast_amd.shard: count all-gather, then the valid
+records point-to-point to rank 0).  The CPU oracle stands in for the GPU env here; the
 GPU runs use the same shard offsets and the same gather over RCCL."""
 import os
 import socket
@@ -70,12 +71,14 @@ def test_two_rank_shards_equal_one_big_run(tmp_path):
 
 
 def _async_worker(rank, world, port, result_path):
-    """AsyncTransitionGather: double-buffered all-gathers issued asynchronously per launch."""
+    """AsyncTransitionGather: count all-gather per launch, then (one launch later) the valid records
+    point-to-point to the learner (rank 0); every record arrives once, none is dropped."""
     from sac_maritime_ast_amd.shard import AsyncTransitionGather
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         g = AsyncTransitionGather(16, 24, torch.float64, "cpu", world)
+        seen = []
         for i in range(5):
             rec, cnt = g.buffers(i)
             n = 3 + i + rank                       # rank- and launch-dependent record counts
@@ -84,20 +87,53 @@ def _async_worker(rank, world, port, result_path):
             rec[:n, 23] = float(rank)
             cnt.fill_(n)
             g.start(i)
-            if i == 3:
-                got = g.records(i)
-                assert got.shape[0] == sum(3 + i + r for r in range(world))
-                assert torch.all(got[:, 0] == i)
-                for r in range(world):
-                    assert int((got[:, 23] == r).sum()) == 3 + i + r
+            g.progress(i - 1)
+            if rank == 0 and i > 0:
+                seen.append((i - 1, g.records(i - 1).clone()))
         g.finish()
-        assert g.launches == 5
+        if rank == 0:
+            seen.append((4, g.records(4).clone()))
+            for j, got in seen:
+                assert got.shape[0] == sum(3 + j + r for r in range(world))
+                assert torch.all(got[:, 0] == j)
+                for r in range(world):
+                    assert int((got[:, 23] == r).sum()) == 3 + j + r
+        assert g.launches == 5 and g.dropped() == 0
+        assert g.gathered == sum(3 + j + r for j in range(5) for r in range(world))
         if rank == 0:
             with open(result_path, "w") as f:
                 f.write("ok")
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+def _overflow_worker(rank, world, port, result_path):
+    """Records beyond a rank's capacity are counted as dropped, the rest still arrive."""
+    from sac_maritime_ast_amd.shard import AsyncTransitionGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = AsyncTransitionGather(8, 24, torch.float64, "cpu", world)
+        rec, cnt = g.buffers(0)
+        rec[:, 23] = float(rank)
+        cnt.fill_(8 + 5 * rank)                    # rank 1 wrote 13 > capacity 8
+        g.start(0)
+        g.finish()
+        assert g.dropped() == 5 and g.gathered == 16
+        if rank == 0:
+            assert g.records(0).shape[0] == 16
+            with open(result_path, "w") as f:
+                f.write("ok")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_transition_gather_counts_overflow(tmp_path):
+    path = str(tmp_path / "result_overflow.txt")
+    mp.spawn(_overflow_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    assert open(path).read() == "ok"
 
 
 def test_async_transition_gather_two_ranks(tmp_path):

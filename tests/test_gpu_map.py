@@ -9,8 +9,11 @@ reproduce the full scans of the reference's predicates exactly:
 Points: uniform over the map and its margin, dense bands along every edge (offsets from 1e-9 m
 to 80 m on both sides), exact vertices, edge midpoints, and rays through vertex latitudes
 (GEOS's degenerate cases).  float64: identical booleans everywhere, distance within 1e-12.
-float32: identical booleans except within 5 cm of a boundary (float32 coordinate rounding at
-1e4 m is ~5e-4 m; such points are counted and bounded), distance within 1e-5 relative (floor 10 m).
+float32 (the probes run in the float32 step kernels' translation unit, device fast-math): the
+oracle evaluates the same float32 points in float64; containment and the hull test are identical
+everywhere, on the boundary band included — the kernel decides containment in float64 from the
+float32 point (count_segment) and forms the hull corners n +- l/2 in float64 as the reference
+does — and the distance is within 1e-5 relative (floor 10 m).
 """
 import numpy as np
 import pytest
@@ -112,8 +115,9 @@ def test_f32_map_predicates(points):
     # (the reward uses d / 1e6, so this is 1e-10 of reward)
     err = np.abs(dist.astype(np.float64) - d_ref) / np.maximum(d_ref, 10.0)
     assert err.max() <= 1e-5, f"distance rel err {err.max():.3e}"
-    bad = inside != in_ref
-    assert np.all(d_ref[bad] < 0.05), f"contains mismatch {bad.sum()} off the float32 band"
-    bad_h = hull != hull_ref
-    assert np.all(corner_margin(p[bad_h]) < 0.05), f"hull mismatch {bad_h.sum()} off the float32 band"
-    print(f"float32 band mismatches: contains {bad.sum()}, hull {bad_h.sum()} of {len(p)} probes")
+    bad = np.nonzero(inside != in_ref)[0]
+    assert bad.size == 0, f"{bad.size} contains mismatches, e.g. {p[bad[:5]].tolist()}"
+    bad_h = np.nonzero(hull != hull_ref)[0]
+    assert bad_h.size == 0, f"{bad_h.size} hull mismatches, e.g. {p[bad_h[:5]].tolist()}"
+    near = int((corner_margin(p) < 0.05).sum())
+    print(f"float32 probes: {len(p)} points, {near} within 5 cm of a boundary (hull corners included), 0 mismatches")

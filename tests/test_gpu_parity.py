@@ -168,20 +168,18 @@ def test_f32_teacher_forced_vs_oracle():
         worst["next_state"] = max(worst.get("next_state", 0), e.max())
         # reward: terms up to 2000 plus O(1) shaping; tolerance 1e-5 * max(|r|, 1)
         e = rel_err(rew, rew_r, 1.0)
-        ok = (done == done_r) & (stat == st_r)
-        worst["reward"] = max(worst.get("reward", 0), e[ok].max())
-        n_disc += int((~ok).sum())
+        worst["reward"] = max(worst.get("reward", 0), e.max())
+        n_disc += int(((done != done_r) | (stat != st_r)).sum())
         post = np_state(env32)
         ref = o.get_state()
         for k in so.SHIP_REAL:
-            err = rel_err(post[k], ref[k], SCALE[k])[:, ok].max()
-            worst[k] = max(worst.get(k, 0), err)
-        for k in ("next_wpt", "n_wpt"):
+            worst[k] = max(worst.get(k, 0), rel_err(post[k], ref[k], SCALE[k]).max())
+        for k in ("next_wpt", "n_wpt", "stop"):
             assert np.array_equal(post[k], ref[k]), f"depth {depth}: {k}"
     print("f32 teacher-forced worst:", {k: f"{v:.2e}" for k, v in worst.items()}, "discrete mismatches:", n_disc)
     for k, v in worst.items():
         assert v <= 1e-5, f"{k}: {v:.3e}"
-    assert n_disc <= 3, f"{n_disc} discrete mismatches (float32 knife edges)"
+    assert n_disc == 0, f"{n_disc} done/status mismatches"
 
 
 # ------------------------------------------------------------------------------------------
@@ -410,3 +408,165 @@ def test_f32_rollout_log_sanity():
     ns = out["next_state"]
     same = ~out["done"][:-1].bool()
     assert torch.equal(log[1:, 1][same], ns[:-1, :, 0][same])
+
+
+# ------------------------------------------------------------------------------------------
+# float32: the benchmarked instantiation (k_env_steps<float, kSynth, LDS map, no log>, device
+# fast-math) — one fused step from float32 states at six depths of an episode
+# ------------------------------------------------------------------------------------------
+def f32_rounded(st):
+    return {k: (v.astype(np.float32).astype(np.float64) if v.dtype == np.float64 else v) for k, v in st.items()}
+
+
+def test_f32_synthetic_rollout_step_vs_oracle():
+    """rollout(1) in synthetic-sampler mode with auto-reset — the kernel and flags the bench times —
+    from float32-rounded states of 4096 envs at six episode depths, against OracleEnvs.rollout(1)
+    on the same state: next_state, reward, IW actions and the post-state within 1e-5 relative
+    (per-field floors); done, status, sampling events, waypoint index, route length, stop flags,
+    episode counters and the replay transitions' discrete fields identical."""
+    n_env = 4096
+    sc = make_scenario(n_env, cap=32)
+    env64 = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+    env64.reset()
+    env64.init_step()
+    env32 = VecMultiShipRLEnv(scenario=sc, precision=32, device=DEV)
+    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+    worst, n_done, n_sac = {}, 0, 0
+
+    def upd(k, v):
+        worst[k] = max(worst.get(k, 0.0), float(v))
+    for depth in range(6):
+        env64.rollout(300, seed=21 + depth)
+        st32 = f32_rounded(np_state(env64))
+        o.set_state(st32)
+        env32.set_state(st32)
+        seed = 900 + depth
+        r = o.rollout(1, seed=seed, mask_horizon=600)
+        out = env32.rollout(1, seed=seed, transition_capacity=2 * n_env, mask_horizon=600)
+        ns, rew = out["next_state"][0].cpu().numpy(), out["reward"][0].cpu().numpy()
+        upd("next_state", rel_err(ns, r["next_state"][0], OBS_SCALE).max())
+        upd("reward", rel_err(rew, r["reward"][0], 1.0).max())
+        done = out["done"][0].cpu().numpy().astype(bool)
+        stat = out["status"][0].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        assert np.array_equal(done, r["done"][0]), f"depth {depth}: done"
+        assert np.array_equal(stat, r["status"][0].astype(np.int64)), f"depth {depth}: status"
+        n_done += int(done.sum())
+        act = out["action"][0].cpu().numpy().astype(np.float64)
+        sac = r["action"][0, :, 3] > 0.5
+        n_sac += int(sac.sum())
+        assert np.array_equal(act[:, 3] > 0.5, sac), f"depth {depth}: sampling events"
+        upd("iw", rel_err(act[sac, :2], r["action"][0, sac, :2], 1e4).max() if sac.any() else 0.0)
+        post, ref = np_state(env32), o.get_state()
+        for k in so.SHIP_REAL:
+            upd(k, rel_err(post[k], ref[k], SCALE[k]).max())
+        for k in ("sampling_dist", "eps_dist", "prev_pre_north", "prev_pre_east", "iw_north", "iw_east"):
+            upd(k, rel_err(post[k], ref[k], SCALE[k]).max())
+        for k in so.SHIP_INT + ("ep_step", "event", "episodes"):
+            assert np.array_equal(post[k].astype(np.int64), ref[k].astype(np.int64)), f"depth {depth}: {k}"
+        cnt = int(out["transition_count"].item())
+        got, want = out["transitions"][:cnt].cpu().numpy().astype(np.float64), r["transitions"]
+        assert cnt == len(want), f"depth {depth}: transitions {cnt} vs {len(want)}"
+        if cnt:
+            got, want = got[np.argsort(got[:, 23])], want[np.argsort(want[:, 23])]
+            assert np.array_equal(got[:, 23], want[:, 23]) and np.array_equal(got[:, 22], want[:, 22])
+            assert np.abs(got[:, 10] - want[:, 10]).max() <= 1e-6      # the SAC action in [-1, 1]
+            cols = np.r_[0:10, 12:22]
+            upd("transitions", rel_err(got[:, cols], want[:, cols], np.r_[OBS_SCALE, OBS_SCALE]).max())
+    print("f32 benchmarked-kernel step worst:", {k: f"{v:.2e}" for k, v in worst.items()},
+          f"done {n_done}, sampling events {n_sac}")
+    bad = {k: f"{v:.2e}" for k, v in worst.items() if v > 1e-5}
+    assert not bad, bad
+    assert n_sac > 0
+
+
+def test_f32_free_running_deviation_report():
+    """Reported, not gated: float32 vs float64 free-running from the same start, 4096
+    envs x 2000 steps of the synthetic sampler with auto-reset.  Per env the trajectories agree
+    until the first step whose discrete outputs differ (float32 state drift moving a decision);
+    printed: envs diverged, the earliest divergence, and the largest next_state deviation before it."""
+    n_env, steps, chunk = 4096, 2000, 500
+    sc = make_scenario(n_env, cap=48)
+    envs = [VecMultiShipRLEnv(scenario=sc, precision=p, device=DEV) for p in (32, 64)]
+    for e in envs:
+        e.reset()
+        e.init_step()
+    first = np.full(n_env, steps)
+    dev_max = np.zeros(n_env)
+    rew_max = np.zeros(n_env)
+    for k0 in range(0, steps, chunk):
+        o32, o64 = (e.rollout(chunk, seed=77) for e in envs)
+        d32, d64 = o32["done"].cpu().numpy(), o64["done"].cpu().numpy()
+        s32 = o32["status"].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        s64 = o64["status"].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        a32, a64 = o32["action"][..., 3].cpu().numpy(), o64["action"][..., 3].cpu().numpy()
+        diff = (d32 != d64) | (s32 != s64) | (a32 != a64)
+        step_idx = np.where(diff.any(0), diff.argmax(0) + k0, steps)
+        first = np.minimum(first, step_idx)
+        ok = (np.arange(k0, k0 + chunk)[:, None] < first[None, :])
+        e = rel_err(o32["next_state"].cpu().numpy(), o64["next_state"].cpu().numpy(), OBS_SCALE).max(-1)
+        dev_max = np.maximum(dev_max, np.where(ok, e, 0).max(0))
+        er = rel_err(o32["reward"].cpu().numpy(), o64["reward"].cpu().numpy(), 1.0)
+        rew_max = np.maximum(rew_max, np.where(ok, er, 0).max(0))
+    div = first < steps
+    print(f"f32 vs f64 free-running, {n_env} envs x {steps} steps: {int(div.sum())} envs diverged "
+          f"(earliest step {int(first.min()) if div.any() else None}, median {float(np.median(first[div])) if div.any() else None}); "
+          f"before divergence max next_state rel dev {dev_max.max():.2e} (median env {np.median(dev_max):.2e}), "
+          f"max reward dev {rew_max.max():.2e}")
+    assert np.isfinite(dev_max).all()
+
+
+# ------------------------------------------------------------------------------------------
+# sharding: envs are independent units keyed by global env id (SURVEY §8(e))
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("precision", [64, 32])
+def test_two_shards_equal_one_handle(precision):
+    """Two handles with env_id_offset 0 and n reproduce one 2n-env handle bit for bit (the path the
+    multi-GPU bench runs on every rank), including the replay transitions."""
+    n, steps = 1024, 400
+    outs = []
+    for parts in (((0, 2 * n),), ((0, n), (n, n))):
+        res = []
+        for off, cnt in parts:
+            env = VecMultiShipRLEnv(scenario=make_scenario(cnt, cap=48, env_offset=off), precision=precision,
+                                    device=DEV)
+            env.reset()
+            env.init_step()
+            o = env.rollout(steps, seed=31, env_id_offset=off, transition_capacity=4 * cnt)
+            tr = o["transitions"][:int(o["transition_count"].item())].cpu().numpy()
+            res.append((o["next_state"].cpu().numpy(), o["reward"].cpu().numpy(), o["status"].cpu().numpy(),
+                        tr[np.lexsort((tr[:, 12], tr[:, 23]))]))
+        outs.append(res)
+    (ns, rw, st, tr), = outs[0]
+    cat = [np.concatenate([r[i] for r in outs[1]], axis=1) for i in range(3)]
+    assert np.array_equal(ns, cat[0]) and np.array_equal(rw, cat[1]) and np.array_equal(st, cat[2])
+    tr2 = np.concatenate([r[3] for r in outs[1]])
+    tr2 = tr2[np.lexsort((tr2[:, 12], tr2[:, 23]))]
+    assert np.array_equal(tr, tr2, equal_nan=True)
+
+
+# ------------------------------------------------------------------------------------------
+# the float64 helpers of the knife-edge decisions, as compiled in both translation units
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("fast_tu", [1, 0])
+def test_ieee_f64_helpers_bitwise(fast_tu):
+    rng = np.random.default_rng(5)
+    n = 1 << 16
+    a = np.concatenate([rng.uniform(-1e4, 1e4, n).astype(np.float32).astype(np.float64),
+                        rng.uniform(0, 1, n) * 10.0 ** rng.integers(-300, 300, n),
+                        [0.0, -0.0, 1e-310, 5e-324, 2.0 ** -767, 1e308, 4e4, 1000.0]])
+    b = np.concatenate([rng.uniform(-1e4, 1e4, n).astype(np.float32).astype(np.float64),
+                        rng.uniform(0.5, 2, n) * 10.0 ** rng.integers(-300, 300, n),
+                        [1.0, 3.0, 7.0, 1e-310, 3.0, 1e-308, 200.0, 1000.0]])
+    with np.errstate(all="ignore"):
+        want = [a / b, np.sqrt(np.abs(a)), a * a + b * b, (a + b) - a, a * b + b * a]
+    lib = _lib.load()
+    for op, w in enumerate(want):
+        x = np.abs(a) if op == 1 else a
+        ta, tb = torch.from_numpy(x).to(DEV), torch.from_numpy(b).to(DEV)
+        out = torch.empty_like(ta)
+        _lib.check(lib.sit_selftest_f64(op, len(x), ta.data_ptr(), tb.data_ptr(), out.data_ptr(), fast_tu, None))
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        fin = np.isfinite(w)
+        bad = np.nonzero(got[fin].view(np.int64) != w[fin].view(np.int64))[0]
+        assert bad.size == 0, f"op {op}: {bad.size} results differ, e.g. a={x[fin][bad[:3]]} b={b[fin][bad[:3]]}"

@@ -98,8 +98,9 @@ def test_f64_policy_mode_matches_synchronous_loop(capacity):
     env.reset()
     env.init_step()
     pol = make_policy(torch.float64, DEV)
-    sm = PolicySampler(env, pol, chunk=chunk, seed=SEED, request_capacity=capacity)
-    seq = per_env(run_gpu(sm, n_launch), 0, n_env)
+    sm = PolicySampler(env, pol, chunk=chunk, seed=SEED, request_capacity=capacity, transition_capacity=2 * n_env)
+    rows = run_gpu(sm, n_launch)
+    seq = per_env(rows, 0, n_env)
     done_steps = min(len(r) for r in seq["reward"])
     executed = int(sm.env_steps.item())
     assert executed == sum(len(r) for r in seq["reward"])
@@ -108,6 +109,26 @@ def test_f64_policy_mode_matches_synchronous_loop(capacity):
     compare(seq, ref, n_env, done_steps)
     # the actor saw sampling events of every env (init events at least)
     assert int(sm.served.item()) >= n_env
+    # replay transitions of the policy's events: per env in event order (an env takes at most one
+    # sampling event per launch: it waits for the actor at the next one), the action column holding
+    # the policy's squashed action in [-1, 1] as in synthetic mode (memory.push, main_ast.py:395)
+    gpu = [[] for _ in range(n_env)]
+    for launch in rows:
+        o = launch[0]
+        tr = o["transitions"][:int(o["transition_count"][0])]
+        for rec in tr:
+            gpu[int(rec[23])].append(rec)
+    want = ref["transitions"]
+    assert len(want) >= n_env
+    for e in range(n_env):
+        w = want[want[:, 23] == e]
+        g = np.array(gpu[e][:len(w)])
+        assert len(g) == len(w), f"env {e}: {len(g)} transitions vs {len(w)}"
+        assert np.array_equal(g[:, 22], w[:, 22]), f"env {e}: masks"
+        assert np.abs(g[:, 10]).max() <= 1.0
+        scale = np.r_[OBS_SCALE, 1.0, 1.0, OBS_SCALE]
+        err = np.abs(g[:, :22] - w[:, :22]) / np.maximum(np.abs(w[:, :22]), scale)
+        assert err.max() <= 1e-9, f"env {e}: transition rel err {err.max():.3e}"
 
 
 def test_f64_overlapped_groups_match():
