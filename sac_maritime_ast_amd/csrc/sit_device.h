@@ -115,6 +115,17 @@ template <typename T> __device__ __forceinline__ T xclip(T v, T lo, T hi) { retu
 // --------------------------------------------------------------------------------------
 // constants (derived on the host in double, cast once to T)
 // --------------------------------------------------------------------------------------
+// the float64 values of every threshold and of the gains a knife-edge re-evaluation needs
+// (float32 handle: decisions whose float32 margin lies inside the float32 error band are re-taken
+// in float64 from the float32 state; float64 handle: the decisions themselves).  The step kernel
+// reads them from its LDS copy of the constants inside the rare branches, so they hold no
+// registers across the step loop.
+struct ConstsX64 {
+  double los_r, windup, e_tol, arrival, rpm_max, min_dist, blackout;
+  double dt, kp1, ki1, kp2, ki2, avail_prop, me_cap, hotel, load_el_gen, bias_scale, bias_max;
+  double half_len, theta;
+};
+
 template <typename T>
 struct Consts {
   T dt;
@@ -152,14 +163,7 @@ struct Consts {
   T fx0, fy0, finvx, finvy;   // fine class grid origin and 1 / cell size
   // trajectory log only (store_simulation_data, fuel model)
   T el_cap, fuel_me_a, fuel_me_b, fuel_me_c, fuel_dg_a, fuel_dg_b, fuel_dg_c, rad2deg;
-  // the float64 values of every threshold and of the gains a knife-edge re-evaluation needs
-  // (float32 handle: decisions whose float32 margin lies inside the float32 error band are
-  // re-taken in float64 from the float32 state; float64 handle: the decisions themselves)
-  struct X64 {
-    double los_r, windup, e_tol, arrival, rpm_max, min_dist, blackout;
-    double dt, kp1, ki1, kp2, ki2, avail_prop, me_cap, hotel, load_el_gen, bias_scale, bias_max;
-    double half_len, theta;
-  } x;
+  ConstsX64 x;
 };
 
 // island map (obstacle.py:92-124): edge i of the closed rings runs from (ax, ay) to (bx, by);
@@ -375,24 +379,26 @@ struct Ship {
 // LOS_guidance.py:110-120 in the reference's float64 arithmetic from the (float32) state: the
 // cross-track error |e|, the (clamped) e / Delta and whether the integrator accepts it
 template <typename T>
-__device__ __forceinline__ void los_exact(const Consts<T>& c, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
-                                                    double& ect_abs, double& q, double& sum, bool& accept) {
+__device__ __forceinline__ void los_exact(const ConstsX64& x, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
+                                          double& ect_abs, double& q, double& sum, bool& accept) {
   const double dx = ieee_sub(cn, pn), dy = ieee_sub(ce, pe);
   const double len = ieee_sqrt(ieee_sq2(dx, dy));
   const double sa = len > 0.0 ? ieee_div(dy, len) : 0.0, ca = len > 0.0 ? ieee_div(dx, len) : 1.0;
   double ect = ieee_add(ieee_mul(-ieee_sub(n, pn), sa), ieee_mul(ieee_sub(e, pe), ca));
   ect_abs = fabs(ect);
-  const double r2 = ieee_mul(c.x.los_r, c.x.los_r);
-  if (ieee_mul(ect, ect) >= r2) ect = ieee_mul(0.99, c.x.los_r);
+  const double r2 = ieee_mul(x.los_r, x.los_r);
+  if (ieee_mul(ect, ect) >= r2) ect = ieee_mul(0.99, x.los_r);
   q = ieee_div(ect, ieee_sqrt(ieee_sub(r2, ieee_mul(ect, ect))));
   sum = ieee_add((double)ect_int, q);
-  accept = fabs(sum) <= c.x.windup;
+  accept = fabs(sum) <= x.windup;
 }
 
+// ect_over: |e_ct| > e_tolerance (the navigation-failure predicate, MSRL_env_ex.py:560-576) decided
+// exactly (float64 inside the float32 band)
 template <typename T>
-__device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s, Route<T>& rt,
+__device__ __forceinline__ void guidance_control(const Consts<T>& c, const ConstsX64& x, Ship<T>& s, Route<T>& rt,
                                                  T v_des, T& rudder, T& thr, T& ect_abs, T& psi_ref_out,
-                                                 double& ect_x) {
+                                                 bool& ect_over) {
   // next_wpt: acceptance test evaluated in IEEE float64 from the stored values (the reference's
   // decision for the same state; LOS_guidance.py:96)
   rt.advance(ieee_sq2(ieee_sub(rt.cn, s.n), ieee_sub(rt.ce, s.e)) <= c.ra2 && rt.nw > s.k + 1, s.k);
@@ -400,7 +406,7 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
   const T alpha = rt.alpha, sa = rt.sa, ca = rt.ca;
   T ect = -(s.n - pn) * sa + (s.e - pe) * ca;
   ect_abs = xabs(ect);
-  ect_x = (double)ect_abs;
+  ect_over = ect_abs > c.e_tol;
   bool clamp = ect * ect >= c.los_r2;
   if (clamp) ect = c.los_clamp;                           // sign lost (Q5)
   const T delta = xsqrt(c.los_r2 - ect * ect);
@@ -414,12 +420,15 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
     const bool knife = xmin(xabs(ect_abs - c.los_r), xabs(ect_abs - c.e_tol)) < T(0.05) ||
                        xabs(xabs(sum) - c.windup) < T(0.02);
     if (knife) {
-      double qd, sd;
-      los_exact(c, s.n, s.e, pn, pe, rt.cn, rt.ce, s.ect_int, ect_x, qd, sd, accept);
-      ect_abs = (T)ect_x;
+      double ex, qd, sd;
+      los_exact(x, s.n, s.e, pn, pe, rt.cn, rt.ce, s.ect_int, ex, qd, sd, accept);
+      ect_over = ex > x.e_tol;
+      ect_abs = (T)ex;
       q = (T)qd;
       sum = (T)sd;
     }
+  } else {
+    ect_over = (double)ect_abs > x.e_tol;
   }
   if (accept) s.ect_int = sum;
   const T chi = xatan(-q - s.ect_int * c.los_ki);
@@ -445,24 +454,23 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, Ship<T>& s,
 // float64 arithmetic from the pre-step integrals i1, i2 and surge u; with the collision bias of
 // MSRL_Env.py:244-251 when `bias`
 template <typename T>
-__device__ __forceinline__ double throttle_exact(const Consts<T>& c, T u, T v_des, T i1, T i2, bool bias) {
+__device__ __forceinline__ double throttle_exact(const ConstsX64& x, T u, T v_des, T i1, T i2, bool bias) {
   const double e1 = ieee_sub(v_des, u);
-  const double ii1 = ieee_add(i1, ieee_mul(e1, c.x.dt));
-  const double wdes = ieee_dot2(e1, c.x.kp1, ii1, c.x.ki1);
+  const double ii1 = ieee_add(i1, ieee_mul(e1, x.dt));
+  const double wdes = ieee_dot2(e1, x.kp1, ii1, x.ki1);
   const double e2 = ieee_sub(wdes, u);
-  const double ii2 = ieee_add(i2, ieee_mul(e2, c.x.dt));
-  double thr = ieee_dot2(e2, c.x.kp2, ii2, c.x.ki2);
-  if (bias) thr = fmax(0.0, fmin(ieee_mul(thr, c.x.bias_scale), c.x.bias_max));
+  const double ii2 = ieee_add(i2, ieee_mul(e2, x.dt));
+  double thr = ieee_dot2(e2, x.kp2, ii2, x.ki2);
+  if (bias) thr = fmax(0.0, fmin(ieee_mul(thr, x.bias_scale), x.bias_max));
   return thr;
 }
 
 // distribute_load(...).load_on_main_engine / 1000 in float64 (ship_engine.py:46-76)
-template <typename T>
-__device__ __forceinline__ double power_me_kw_exact(const Consts<T>& c, double thr) {
-  const double total = ieee_mul(thr, c.x.avail_prop);
+__device__ __forceinline__ double power_me_kw_exact(int sg_mode, const ConstsX64& x, double thr) {
+  const double total = ieee_mul(thr, x.avail_prop);
   double load_me;
-  if (c.sg_mode == 0) load_me = fmin(total, c.x.me_cap);
-  else if (c.sg_mode == 1) load_me = ieee_sub(ieee_add(total, c.x.hotel), c.x.load_el_gen);
+  if (sg_mode == 0) load_me = fmin(total, x.me_cap);
+  else if (sg_mode == 1) load_me = ieee_sub(ieee_add(total, x.hotel), x.load_el_gen);
   else load_me = total;
   return ieee_div(load_me, 1000.0);
 }
@@ -470,19 +478,19 @@ __device__ __forceinline__ double power_me_kw_exact(const Consts<T>& c, double t
 // is_mechanical_failure (MSRL_env_ex.py:554-558): |shaft speed * 30 / pi| > shaft_rpm_max, with
 // rpm = w * 30 / pi (ship_model.py:652) re-taken in float64 near the threshold
 template <typename T>
-__device__ __forceinline__ bool rpm_fails(const Consts<T>& c, T w, T rpm) {
+__device__ __forceinline__ bool rpm_fails(const Consts<T>& c, const ConstsX64& x, T w, T rpm) {
   if constexpr (kIsF32<T>) {
-    if (xabs(xabs(rpm) - c.rpm_max) < T(0.01)) return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > c.x.rpm_max;
+    if (xabs(xabs(rpm) - c.rpm_max) < T(0.01)) return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > x.rpm_max;
     return xabs(rpm) > c.rpm_max;
   } else {
-    return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > c.x.rpm_max;
+    return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > x.rpm_max;
   }
 }
 
 // sqrt(dn^2 + de^2) <= r (arrival, MSRL_env_ex.py:754, 829) / dn^2 + de^2 < r^2 (collision, :592)
 // as the reference evaluates them in float64, decided in float32 away from the boundary
 template <typename T>
-__device__ __forceinline__ bool within_radius(T n0, T e0, T n1, T e1, T r, double r_x) {
+__device__ __forceinline__ bool within_radius(T n0, T e0, T n1, T e1, T r, const double& r_x) {
   if constexpr (kIsF32<T>) {
     const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de, r2 = r * r;
     if (xabs(d2 - r2) > T(1e-4) * r2) return d2 <= r2;
@@ -490,7 +498,7 @@ __device__ __forceinline__ bool within_radius(T n0, T e0, T n1, T e1, T r, doubl
   return ieee_sqrt(ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1))) <= r_x;
 }
 template <typename T>
-__device__ __forceinline__ bool closer_than(T n0, T e0, T n1, T e1, T r2, double r_x) {
+__device__ __forceinline__ bool closer_than(T n0, T e0, T n1, T e1, T r2, const double& r_x) {
   if constexpr (kIsF32<T>) {
     const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de;
     if (xabs(d2 - r2) > T(1e-4) * r2) return d2 < r2;
@@ -828,6 +836,7 @@ __device__ bool pip_point(const Consts<T>& c, const Map<T>& m, T n, T e) {
 // corners share the centre's side and one point test decides.
 template <typename T>
 __device__ bool hull_corners(const Consts<T>& c, const Map<T>& m, T n, T e);
+
 
 template <typename T>
 __device__ bool hull_in_terrain(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst) {

@@ -223,11 +223,12 @@ __device__ __forceinline__ void reset_ship(const Scen<T>& sc, int type, int env,
 
 // one guidance/control/update/integrate cycle without store, time or bias (MSRL_Env.py:190-217)
 template <typename T>
-__device__ __forceinline__ void init_step_ship(const Consts<T>& c, Ship<T>& s, Route<T>& rt, T v_des) {
+__device__ __forceinline__ void init_step_ship(const Consts<T>& c, const ConstsX64& x, Ship<T>& s, Route<T>& rt,
+                                               T v_des) {
   T rudder, thr, ect, sp, cp, psi_ref;
-  double ect_x;
+  bool ect_over;
   xsincos(s.psi, &sp, &cp);
-  guidance_control(c, s, rt, v_des, rudder, thr, ect, psi_ref, ect_x);
+  guidance_control(c, x, s, rt, v_des, rudder, thr, ect, psi_ref, ect_over);
   ship_dynamics(c, s, thr, rudder, sp, cp);
   rt.fixup(s.k);
 }
@@ -421,7 +422,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   bool iw_valid = false, iw_in = false;
   int ep_step = 0;
   uint32_t event = 0, episodes = 0;
-  double ab_len = 0.0, ab_alpha = 0.0;
+  double ab_len = 0.0, ab_alpha = 0.0, samp_limit = 0.0;
   T lo[6] = {};                      // this ship's part of the last observation
   const int lo_base = type == 0 ? 0 : 6, lo_n = type == 0 ? 6 : 4;
   // policy mode: both lanes of an env track whether its next step is a sampling event
@@ -454,6 +455,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
       episodes = a.st.episodes[env];
       ab_len = a.sc.ab_len[env];
       ab_alpha = a.sc.ab_alpha[env];
+      samp_limit = ieee_mul(ab_len, cs.x.theta);   // is_obs_ship_navigation_failure (MSRL_env_ex.py:569)
     }
   }
   const T maxn = c.max_n;
@@ -508,7 +510,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     double ang = 0.0;                  // the sampled angle; has_ang: drawn on device this step
     double act_n = 0.0;                // the SAC action of the event: ang / (pi / 6), in [-1, 1]
     bool has_ang = false;
-    double ect_x = 0.0;                // |e_ct| for the navigation-failure decision (exact, see guidance_control)
+    bool ect_over = false;             // |e_ct| > e_tolerance, decided exactly (guidance_control)
     bool mech = false, blk = false;    // test ship: mechanical / blackout failure (decided pre-integration)
     bool stall_now = false;
     if (MODE == kPolicy && act && !stalled && need && !ready) {
@@ -568,7 +570,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           }
           s.ticks += 2;                  // stop path: next_time() twice, no integration (Q10)
           o_rpm = s.lrpm; o_ect = s.lect; o_pme = s.lpme;
-          ect_x = (double)o_ect;
+          ect_over = (double)o_ect > cs.x.e_tol;
         } else {
           if (sac) {                     // update_route: insert at index -1 (Q16)
             if (!rt.insert(iwn, iwe, s.k, a.cap)) bits |= SIT_ST_ROUTE_OVERFLOW;
@@ -576,7 +578,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           }
           const T pre_n = s.n, pre_e = s.e;
           T rudder, thr, psi_ref;
-          guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_x);
+          guidance_control(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
           o_rpm = s.w * c.rpm_k;
           o_pme = power_me_kw(c, thr);
           s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
@@ -598,7 +600,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
         const T i1_0 = s.i1, i2_0 = s.i2;   // pre-step integrals (blackout knife edge)
-        guidance_control(c, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_x);
+        guidance_control(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
         if (c.collision_bias) {          // is_collision_imminent() on all-zero states (Q1)
           thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
           rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
@@ -607,10 +609,11 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         o_pme = power_me_kw(c, thr);
         // failure predicates on pre-integration values (MSRL_env_ex.py:554-558, 578-582), exact:
         // float64 where the float32 margin is inside the float32 band (always for the float64 handle)
-        mech = rpm_fails(c, s.w, o_rpm);
+        mech = rpm_fails(c, cs.x, s.w, o_rpm);
         blk = o_pme > c.blackout_kw;
         if (!kIsF32<T> || xabs(o_pme - c.blackout_kw) <= T(1e-4) * (xabs(o_pme) + T(1)))
-          blk = power_me_kw_exact(c, throttle_exact(c, s.u, v_des, i1_0, i2_0, c.collision_bias != 0)) > c.x.blackout;
+          blk = power_me_kw_exact(c.sg_mode, cs.x, throttle_exact(cs.x, s.u, v_des, i1_0, i2_0, c.collision_bias != 0)) >
+                cs.x.blackout;
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
         if (p_lg) store_log_row(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
         ship_dynamics(c, s, thr, rudder, sp, cp);
@@ -637,7 +640,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #ifdef SIT_DIAG_PATHS
       diag_lane(c, map, s.n, s.e, dobst, type == 1, iwn, iwe, dv);
 #endif
-      const bool arrive = within_radius(s.n, s.e, rt.end_n, rt.end_e, c.arrival_radius, c.x.arrival);
+      const bool arrive = within_radius(s.n, s.e, rt.end_n, rt.end_e, c.arrival_radius, cs.x.arrival);
       const bool horizon = outside(c, s.n, s.e, c.half_len);
       int stop = s.stop;
       bool done = false;
@@ -649,7 +652,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           t[row_step] = (T(1) - dobst / c.max_n) / T(100);
           t[2 * row_step] = r_nt;
         }
-        const bool pred[6] = {arrive, horizon, terrain, mech, ect_x > c.x.e_tol, blk};
+        const bool pred[6] = {arrive, horizon, terrain, mech, ect_over, blk};
         const T rew[6] = {T(0), T(0), T(1000), T(1000), T(1000), T(1000)};
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -691,7 +694,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
           stop = 1; done = true;
           bits |= SIT_ST_OBS_IW_TERMINAL;
         }
-        if (ect_x > c.x.e_tol || (double)samp > ieee_mul(ab_len, c.x.theta)) {
+        if (ect_over || (double)samp > samp_limit) {
           if (!stop) r_term = r_term - T(1000);
           stop = 1; done = true;
           bits |= SIT_ST_OBS_NAVIGATION;
@@ -729,7 +732,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     }
     if (live) {
       const T dn = x.n[0][lane] - x.n[1][lane], de = x.e[0][lane] - x.e[1][lane];
-      const bool coll = closer_than(x.n[0][lane], x.e[0][lane], x.n[1][lane], x.e[1][lane], c.min_dist2, c.x.min_dist);
+      const bool coll = closer_than(x.n[0][lane], x.e[0][lane], x.n[1][lane], x.e[1][lane], c.min_dist2, cs.x.min_dist);
       const uint32_t bt = x.bits[0][lane], bo = x.bits[1][lane];
       env_done = ((bt | bo) & kDoneBit) || coll;
       if (coll) s.stop = 1;
@@ -810,7 +813,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         ep_step = 0;
         if (type == 1) { samp = T(0); eps = T(0); ++episodes; }
         for (int j = 0; j < 6; ++j) lo[j] = lo0[j];
-        init_step_ship(c, s, rt, v_des);
+        init_step_ship(c, cs.x, s, rt, v_des);
       }
     }
     SIT_PH(6);
@@ -894,7 +897,7 @@ __global__ __launch_bounds__(256) void k_init_step(const KArgs<T> a, const uint8
   rt.te = a.st.we + (size_t)type * a.cap * n_env + env;
   rt.stride = n_env;
   rt.load_leg(s.k);
-  init_step_ship(a.c, s, rt, init_val(a.sc, type, SIT_INIT_DESIRED_SPEED, env, n_env));
+  init_step_ship(a.c, a.c.x, s, rt, init_val(a.sc, type, SIT_INIT_DESIRED_SPEED, env, n_env));
   store_ship(a.st, sid, s);
 }
 
