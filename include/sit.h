@@ -248,7 +248,8 @@ int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint
                   uint8_t* hull, void* stream);
 /* Self-test of the IEEE float64 helpers the knife-edge decisions use (diagnostic; no reference
  * counterpart): out[i] = op(a[i], b[i]) with op 0 a / b, 1 sqrt(a), 2 a*a + b*b, 3 (a + b) - a,
- * 4 a*b + b*a, each correctly rounded per operation (numpy's float64).  fast_tu != 0 runs the copy
+ * 4 a*b + b*a (each correctly rounded per operation, as numpy's float64), 5 sin(a), 6 cos(a),
+ * 7 atan2(a, b) (the device math library the float64 path uses).  fast_tu != 0 runs the copy
  * compiled with the float32 step kernels' fast-math flags.  Device pointers. */
 int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, double* out, int32_t fast_tu,
                      void* stream);

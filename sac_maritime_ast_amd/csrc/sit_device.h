@@ -5,7 +5,7 @@
 // where a closed form replaces a numpy construct the comment names the reference line:
 //   rotation inverse / mass-matrix inverse      ship_model.py:252-255, 590-603 (closed forms)
 //   wind load, gamma = -atan2(v_rw, u_rw)         ship_model.py:211-231 (trig-free identity)
-//   LOS sin/cos(atan2(dy, dx))                    LOS_guidance.py:110-113 (dy/L, dx/L)
+//   LOS sin/cos(atan2(dy, dx))                    LOS_guidance.py:110-113 (float32: dy/L, dx/L)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -271,14 +271,23 @@ __device__ __forceinline__ double sampler_normal(uint64_t seed, uint64_t env_id,
 // their geometry, so the waypoint switch of a step is a register select (no branch around a
 // table read in the step's instruction stream); the next target is refilled by fixup() at the
 // end of the step.  The table is written only by an insertion, so it stays in HBM.
+// The leg's path-tangential angle and its sine and cosine (LOS_guidance.py:110-113).  float64: the
+// reference's own sin(atan2(dy, dx)), cos(atan2(dy, dx)) (computed once per leg), so the
+// cross-track error and the clamp decision |e_ct| >= lookahead follow the reference to the last
+// bit; float32: dy / L, dx / L (the same values within float32 rounding; knife edges of the clamp
+// are re-taken in float64 by los_exact).
 template <typename T>
 __device__ __forceinline__ void leg_geom(T pn, T pe, T cn, T ce, T& alpha, T& sa, T& ca) {
   const T dx = cn - pn, dy = ce - pe;
   alpha = xatan2(dy, dx);
-  const T len = xsqrt(dx * dx + dy * dy);
-  sa = T(0);
-  ca = T(1);
-  if (len > T(0)) { sa = dy / len; ca = dx / len; }
+  if constexpr (kIsF32<T>) {
+    const T len = xsqrt(dx * dx + dy * dy);
+    sa = T(0);
+    ca = T(1);
+    if (len > T(0)) { sa = dy / len; ca = dx / len; }
+  } else {
+    xsincos(alpha, &sa, &ca);
+  }
 }
 
 template <typename T>
@@ -382,8 +391,8 @@ template <typename T>
 __device__ __forceinline__ void los_exact(const ConstsX64& x, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
                                           double& ect_abs, double& q, double& sum, bool& accept) {
   const double dx = ieee_sub(cn, pn), dy = ieee_sub(ce, pe);
-  const double len = ieee_sqrt(ieee_sq2(dx, dy));
-  const double sa = len > 0.0 ? ieee_div(dy, len) : 0.0, ca = len > 0.0 ? ieee_div(dx, len) : 1.0;
+  double sa, ca;
+  sincos(atan2(dy, dx), &sa, &ca);                  // math.sin / math.cos of math.atan2 (:110-113)
   double ect = ieee_add(ieee_mul(-ieee_sub(n, pn), sa), ieee_mul(ieee_sub(e, pe), ca));
   ect_abs = fabs(ect);
   const double r2 = ieee_mul(x.los_r, x.los_r);

@@ -73,7 +73,7 @@ int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint
 
 int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, double* out, int32_t fast_tu,
                      void* stream) {
-  if (op < 0 || op > 4 || n < 0 || (n > 0 && (!a || !b || !out))) return SIT_E_INVALID;
+  if (op < 0 || op > 7 || n < 0 || (n > 0 && (!a || !b || !out))) return SIT_E_INVALID;
   if (n == 0) return SIT_OK;
   return fast_tu ? launch_selftest_f32tu(op, n, a, b, out, stream)
                  : launch_selftest(op, n, a, b, out, (hipStream_t)stream);

@@ -499,19 +499,21 @@ def test_f32_free_running_deviation_report():
         s32 = o32["status"].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
         s64 = o64["status"].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
         a32, a64 = o32["action"][..., 3].cpu().numpy(), o64["action"][..., 3].cpu().numpy()
-        diff = (d32 != d64) | (s32 != s64) | (a32 != a64)
+        e = rel_err(o32["next_state"].cpu().numpy(), o64["next_state"].cpu().numpy(), OBS_SCALE).max(-1)
+        # divergence: a discrete output differs, or the state jumps apart (> 1e-3: a waypoint switch
+        # or an episode event one step earlier or later)
+        diff = (d32 != d64) | (s32 != s64) | (a32 != a64) | (e > 1e-3)
         step_idx = np.where(diff.any(0), diff.argmax(0) + k0, steps)
         first = np.minimum(first, step_idx)
         ok = (np.arange(k0, k0 + chunk)[:, None] < first[None, :])
-        e = rel_err(o32["next_state"].cpu().numpy(), o64["next_state"].cpu().numpy(), OBS_SCALE).max(-1)
         dev_max = np.maximum(dev_max, np.where(ok, e, 0).max(0))
         er = rel_err(o32["reward"].cpu().numpy(), o64["reward"].cpu().numpy(), 1.0)
         rew_max = np.maximum(rew_max, np.where(ok, er, 0).max(0))
     div = first < steps
     print(f"f32 vs f64 free-running, {n_env} envs x {steps} steps: {int(div.sum())} envs diverged "
           f"(earliest step {int(first.min()) if div.any() else None}, median {float(np.median(first[div])) if div.any() else None}); "
-          f"before divergence max next_state rel dev {dev_max.max():.2e} (median env {np.median(dev_max):.2e}), "
-          f"max reward dev {rew_max.max():.2e}")
+          f"before divergence next_state rel dev max {dev_max.max():.2e}, p99 {np.percentile(dev_max, 99):.2e}, "
+          f"median {np.median(dev_max):.2e}; reward dev max {rew_max.max():.2e}")
     assert np.isfinite(dev_max).all()
 
 
@@ -570,3 +572,30 @@ def test_ieee_f64_helpers_bitwise(fast_tu):
         fin = np.isfinite(w)
         bad = np.nonzero(got[fin].view(np.int64) != w[fin].view(np.int64))[0]
         assert bad.size == 0, f"op {op}: {bad.size} results differ, e.g. a={x[fin][bad[:3]]} b={b[fin][bad[:3]]}"
+
+
+@pytest.mark.parametrize("fast_tu", [1, 0])
+def test_device_transcendentals_vs_reference_libm(fast_tu):
+    """sin, cos and atan2 as the float64 path computes them (device math library) against the
+    functions the reference calls (Python's math module, LOS_guidance.py:110-113), on angles and leg
+    vectors of the map's scale: at most 1 ulp apart, and the count of exact matches reported (a
+    knife-edge decision that hinges on the last bit of these can differ only where they do)."""
+    import math
+    rng = np.random.default_rng(9)
+    n = 1 << 15
+    ang = np.concatenate([rng.uniform(-np.pi, np.pi, n), rng.uniform(-30, 30, n)])
+    dy = np.round(rng.uniform(-1e4, 1e4, 2 * n), rng.integers(0, 4, 2 * n))
+    dx = np.round(rng.uniform(-1e4, 1e4, 2 * n), rng.integers(0, 4, 2 * n))
+    lib = _lib.load()
+    report = {}
+    for op, (a, b, fn) in {5: (ang, ang, math.sin), 6: (ang, ang, math.cos), 7: (dy, dx, math.atan2)}.items():
+        ta, tb = torch.from_numpy(a).to(DEV), torch.from_numpy(b).to(DEV)
+        out = torch.empty_like(ta)
+        _lib.check(lib.sit_selftest_f64(op, len(a), ta.data_ptr(), tb.data_ptr(), out.data_ptr(), fast_tu, None))
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        want = np.array([fn(x, y) if op == 7 else fn(x) for x, y in zip(a, b)])
+        ulps = np.abs(got.view(np.int64) - want.view(np.int64))
+        report[fn.__name__] = (int((ulps == 0).sum()), len(a), int(ulps.max()))
+        assert ulps.max() <= 1, f"{fn.__name__}: {int(ulps.max())} ulp"
+    print("device vs reference libm (exact, total, max ulp):", report)
