@@ -413,16 +413,17 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, const Const
   rt.advance(ieee_sq2(ieee_sub(rt.cn, s.n), ieee_sub(rt.ce, s.e)) <= c.ra2 && rt.nw > s.k + 1, s.k);
   const T pn = rt.pn, pe = rt.pe;
   const T alpha = rt.alpha, sa = rt.sa, ca = rt.ca;
-  T ect = -(s.n - pn) * sa + (s.e - pe) * ca;
-  ect_abs = xabs(ect);
-  ect_over = ect_abs > c.e_tol;
-  bool clamp = ect * ect >= c.los_r2;
-  if (clamp) ect = c.los_clamp;                           // sign lost (Q5)
-  const T delta = xsqrt(c.los_r2 - ect * ect);
-  T q = ect / delta;
-  T sum = s.ect_int + q;
-  bool accept = xabs(sum) <= c.windup;
+  T q, sum;
+  bool accept;
   if constexpr (kIsF32<T>) {
+    T ect = -(s.n - pn) * sa + (s.e - pe) * ca;
+    ect_abs = xabs(ect);
+    ect_over = ect_abs > c.e_tol;
+    if (ect * ect >= c.los_r2) ect = c.los_clamp;         // sign lost (Q5)
+    const T delta = xsqrt(c.los_r2 - ect * ect);
+    q = ect / delta;
+    sum = s.ect_int + q;
+    accept = xabs(sum) <= c.windup;
     // knife edges of the clamp (|e| = lookahead), of the navigation-failure threshold (|e| =
     // e_tolerance) and of the anti-windup limit: float32 carries ~1e-3 m of rounding in e and
     // ~3e-4 in the integral, so inside these bands the decisions are re-taken in float64
@@ -437,7 +438,16 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, const Const
       sum = (T)sd;
     }
   } else {
-    ect_over = (double)ect_abs > x.e_tol;
+    // float64: the reference's operation order (LOS_guidance.py:112-119; no fused multiply-add,
+    // sin/cos of atan2 cached with the leg), so the clamp and windup decisions are its own
+    double e = ieee_add(ieee_mul(-ieee_sub(s.n, pn), sa), ieee_mul(ieee_sub(s.e, pe), ca));
+    ect_abs = fabs(e);
+    ect_over = ect_abs > x.e_tol;
+    const double r2 = ieee_mul(x.los_r, x.los_r);
+    if (ieee_mul(e, e) >= r2) e = ieee_mul(0.99, x.los_r);   // sign lost (Q5)
+    q = ieee_div(e, ieee_sqrt(ieee_sub(r2, ieee_mul(e, e))));
+    sum = ieee_add(s.ect_int, q);
+    accept = fabs(sum) <= x.windup;
   }
   if (accept) s.ect_int = sum;
   const T chi = xatan(-q - s.ect_int * c.los_ki);

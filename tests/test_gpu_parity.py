@@ -584,8 +584,9 @@ def test_device_transcendentals_vs_reference_libm(fast_tu):
     rng = np.random.default_rng(9)
     n = 1 << 15
     ang = np.concatenate([rng.uniform(-np.pi, np.pi, n), rng.uniform(-30, 30, n)])
-    dy = np.round(rng.uniform(-1e4, 1e4, 2 * n), rng.integers(0, 4, 2 * n))
-    dx = np.round(rng.uniform(-1e4, 1e4, 2 * n), rng.integers(0, 4, 2 * n))
+    scale = 10.0 ** rng.integers(0, 4, 2 * n)        # leg vectors with 0-3 decimals, like route points
+    dy = np.round(rng.uniform(-1e4, 1e4, 2 * n) * scale) / scale
+    dx = np.round(rng.uniform(-1e4, 1e4, 2 * n) * scale) / scale
     lib = _lib.load()
     report = {}
     for op, (a, b, fn) in {5: (ang, ang, math.sin), 6: (ang, ang, math.cos), 7: (dy, dx, math.atan2)}.items():

@@ -163,8 +163,8 @@ def test_f64_sim_teacher_forced_vs_reference(case):
     assert np.array_equal(post["next_wpt"][0], _post(d, post_prefix, rows, "next_wpt").astype(np.int64)), \
         f"{name}: waypoint index"
     for k in REAL:
-        e = rel_err(post[k][0], _post(d, post_prefix, rows, k), SCALE[k]).max()
-        assert e <= 1e-9, f"{name} bias={bias}: {k} rel err {e:.3e}"
+        e = rel_err(post[k][0], _post(d, post_prefix, rows, k), SCALE[k])
+        assert e.max() <= 1e-9, f"{name} bias={bias}: {k} rel err {e.max():.3e} at case {rows[e.argmax()]}"
     ns = out["next_state"][0].cpu().numpy()
     for k, col in OBS_COLS.items():
         assert rel_err(ns[:, col], np.asarray(d["out_" + k])[rows], SCALE[k]).max() <= 1e-9, f"{name} {k}"
