@@ -134,7 +134,9 @@ def load():
                           "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:        # diagnostic builds of older revisions (A/B timing) lack newer entries
+            continue
         fn.restype = res
         fn.argtypes = args
     if lib.sit_abi_version() != 1:
