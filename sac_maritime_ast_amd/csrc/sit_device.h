@@ -499,8 +499,9 @@ __device__ __forceinline__ double power_me_kw_exact(int sg_mode, const ConstsX64
 template <typename T>
 __device__ __forceinline__ bool rpm_fails(const Consts<T>& c, const ConstsX64& x, T w, T rpm) {
   if constexpr (kIsF32<T>) {
-    if (xabs(xabs(rpm) - c.rpm_max) < T(0.01)) return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > x.rpm_max;
-    return xabs(rpm) > c.rpm_max;
+    // at or beyond the threshold's float32 band: decided in float64 (rare: a failing shaft)
+    if (xabs(rpm) > c.rpm_max - T(0.01)) return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > x.rpm_max;
+    return false;
   } else {
     return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > x.rpm_max;
   }
@@ -818,20 +819,54 @@ __device__ __forceinline__ int fine_class(const Consts<T>& c, const Map<T>& m, T
   return fine_lookup(c, m, n, e, cell, word);
 }
 
+// float32 fast path of count_segment for a query point q known within 4e-3 m (a float32 position
+// exactly, a float32-rounded hull corner within half an ulp <= 5e-4 m inside the class grid):
+// the float32 decisions equal the exact ones unless a vertex coordinate lies within that
+// tolerance of q's, or the orientation is inside its float32 error band; those cases set `unsure`
+// and the caller re-decides the point in float64 (rare: points within millimetres of a vertex
+// latitude or an edge line)
+__device__ __forceinline__ void count_segment_f32(float p1x, float p1y, float p2x, float p2y, float qx, float qy,
+                                                  uint32_t bit, uint32_t& parity, uint32_t& onb, bool& unsure) {
+  constexpr float tol = 4e-3f;
+  unsure |= xmin(xmin(xabs(p1y - qy), xabs(p2y - qy)), xmin(xabs(p1x - qx), xabs(p2x - qx))) <= tol;
+  if (p1x < qx && p2x < qx) return;
+  const int up1 = p1y > qy, up2 = p2y > qy;
+  const int straddle = (up1 & !up2) | (up2 & !up1);
+  if (straddle) {
+    const float ax = p1x - qx, by = p2y - qy, ay = p1y - qy, bx = p2x - qx;
+    const float dl = ax * by, dr = ay * bx, det = dl - dr;
+    unsure |= xabs(det) <= 1e-5f * (xabs(dl) + xabs(dr)) + tol * (xabs(ax) + xabs(ay) + xabs(bx) + xabs(by));
+    const int o = (det > 0.f) - (det < 0.f);
+    parity ^= (((p2y < p1y) ? -o : o) > 0) ? bit : 0u;
+  }
+  (void)onb;
+}
+
 // Polygon.contains(Point(e, n)) for a point in mixed class cell `cell` (class word `word`):
-// the cell's constant crossing parity plus GEOS's count over the cell's live edges only, at the
-// exact float64 point (n, e)
+// the cell's constant crossing parity plus GEOS's count over the cell's live edges only.  (nd, ed)
+// is the exact float64 point; (n, e) its value in T.  float32: the count runs in float32 and is
+// re-run in float64 only where count_segment_f32 is unsure.
 template <typename T>
-__device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t word, double n, double e) {
+__device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t word, T n, T e, double nd, double ed) {
   const uint32_t mixed = (word >> 1) & 0x55555555u;
   const int r = m.frank[cell >> 4] + __popc(mixed & ((1u << ((cell & 15) * 2)) - 1u));
   const uint2 rec = m.crec[r];
-  uint32_t par = rec.x, onb = 0;
   const int first = (int)(rec.y & 0xffffu), cnt = (int)(rec.y >> 16);
+  if constexpr (kIsF32<T>) {
+    uint32_t par = rec.x, onb = 0;
+    bool unsure = false;
+#pragma unroll 1
+    for (int k = 0; k < cnt; ++k) {
+      const Edge<T> g = m.edge[m.clive[first + k]];
+      count_segment_f32(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb, unsure);
+    }
+    if (!unsure) return par != 0;
+  }
+  uint32_t par = rec.x, onb = 0;
 #pragma unroll 1
   for (int k = 0; k < cnt; ++k) {
     const Edge<T> g = m.edge[m.clive[first + k]];
-    count_segment(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
+    count_segment(g.ax, g.ay, g.bx, g.by, ed, nd, 1u << g.poly, par, onb);
   }
   return (par & ~onb) != 0;
 }
@@ -845,7 +880,7 @@ __device__ bool pip_point(const Consts<T>& c, const Map<T>& m, T n, T e) {
   uint32_t word;
   const int cls = fine_lookup(c, m, n, e, cell, word);
   if (cls < 2) return cls == 1;
-  if (m.use_cells) return pip_cell(m, cell, word, n, e);
+  if (m.use_cells) return pip_cell(m, cell, word, n, e, (double)n, (double)e);
   return pip_indexed(c, m, n, e);
 }
 
@@ -870,7 +905,7 @@ __device__ __forceinline__ bool hull_in_terrain_cls(const Consts<T>& c, const Ma
                                                     int cls, int cell, uint32_t word) {
   if (dobst > c.hull_safe) {
     if (cls < 2) return cls == 1;
-    if (m.use_cells) return pip_cell(m, cell, word, n, e);
+    if (m.use_cells) return pip_cell(m, cell, word, n, e, (double)n, (double)e);
     return pip_indexed(c, m, n, e);
   }
   return hull_corners(c, m, n, e);
@@ -879,24 +914,26 @@ __device__ __forceinline__ bool hull_in_terrain_cls(const Consts<T>& c, const Ma
 template <typename T>
 __device__ bool hull_corners(const Consts<T>& c, const Map<T>& m, T n, T e) {
   const T h = c.half_len;
-  // the corners as the reference forms them (n +- l/2 in float64; exact for a float32 position)
+  // the corners as the reference forms them: n +- l/2 in float64 (exact for a float32 position);
+  // their float32 roundings n -+ h pick the class cells (pure cells have a 1 m margin)
   const double hx = c.x.half_len;
-  const double nlo = ieee_sub(n, hx), nhi = ieee_add(n, hx), elo = ieee_sub(e, hx), ehi = ieee_add(e, hx);
-  // near shore: each corner by its fine-grid class (cell index in T: pure cells have a 1 m margin);
-  // a corner in a mixed cell by the cell's record (or a band scan without records)
+  // near shore: each corner by its fine-grid class; a corner in a mixed cell by the cell's record
+  // (or a band scan without records)
   if (m.use_cells) {
     int l00, l01, l10, l11;
     uint32_t w00, w01, w10, w11;
-    const int c00 = fine_lookup(c, m, n - h, e - h, l00, w00), c01 = fine_lookup(c, m, n - h, e + h, l01, w01);
-    const int c10 = fine_lookup(c, m, n + h, e - h, l10, w10), c11 = fine_lookup(c, m, n + h, e + h, l11, w11);
+    const T nl = n - h, nh = n + h, el = e - h, eh = e + h;
+    const int c00 = fine_lookup(c, m, nl, el, l00, w00), c01 = fine_lookup(c, m, nl, eh, l01, w01);
+    const int c10 = fine_lookup(c, m, nh, el, l10, w10), c11 = fine_lookup(c, m, nh, eh, l11, w11);
     if (c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1) return true;
     bool hit = false;
-    if (c00 == 2) hit |= pip_cell(m, l00, w00, nlo, elo);
-    if (c01 == 2) hit |= pip_cell(m, l01, w01, nlo, ehi);
-    if (c10 == 2) hit |= pip_cell(m, l10, w10, nhi, elo);
-    if (c11 == 2) hit |= pip_cell(m, l11, w11, nhi, ehi);
+    if (c00 == 2) hit |= pip_cell(m, l00, w00, nl, el, ieee_sub(n, hx), ieee_sub(e, hx));
+    if (c01 == 2) hit |= pip_cell(m, l01, w01, nl, eh, ieee_sub(n, hx), ieee_add(e, hx));
+    if (c10 == 2) hit |= pip_cell(m, l10, w10, nh, el, ieee_add(n, hx), ieee_sub(e, hx));
+    if (c11 == 2) hit |= pip_cell(m, l11, w11, nh, eh, ieee_add(n, hx), ieee_add(e, hx));
     return hit;
   }
+  const double nlo = ieee_sub(n, hx), nhi = ieee_add(n, hx), elo = ieee_sub(e, hx), ehi = ieee_add(e, hx);
   const int c00 = fine_class(c, m, n - h, e - h), c01 = fine_class(c, m, n - h, e + h);
   const int c10 = fine_class(c, m, n + h, e - h), c11 = fine_class(c, m, n + h, e + h);
   if (c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1) return true;

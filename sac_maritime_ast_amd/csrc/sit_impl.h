@@ -610,10 +610,13 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
         // failure predicates on pre-integration values (MSRL_env_ex.py:554-558, 578-582), exact:
         // float64 where the float32 margin is inside the float32 band (always for the float64 handle)
         mech = rpm_fails(c, cs.x, s.w, o_rpm);
-        blk = o_pme > c.blackout_kw;
-        if (!kIsF32<T> || xabs(o_pme - c.blackout_kw) <= T(1e-4) * (xabs(o_pme) + T(1)))
-          blk = power_me_kw_exact(c.sg_mode, cs.x, throttle_exact(cs.x, s.u, v_des, i1_0, i2_0, c.collision_bias != 0)) >
-                cs.x.blackout;
+        // MOTOR (PTI): load_me = min(total, ME capacity) <= ME capacity, so no blackout ever (Q7)
+        if (c.sg_mode != SIT_SG_MOTOR) {
+          blk = o_pme > c.blackout_kw;
+          if (!kIsF32<T> || xabs(o_pme - c.blackout_kw) <= T(1e-4) * (xabs(o_pme) + T(1)))
+            blk = power_me_kw_exact(c.sg_mode, cs.x, throttle_exact(cs.x, s.u, v_des, i1_0, i2_0,
+                                                                    c.collision_bias != 0)) > cs.x.blackout;
+        }
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
         if (p_lg) store_log_row(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
         ship_dynamics(c, s, thr, rudder, sp, cp);
