@@ -19,6 +19,13 @@ namespace sit {
 
 template <typename T>
 constexpr bool kIsF32 = std::is_same<T, float>::value;
+// diagnostic builds only (tools/ab2.sh): the float32 knife-edge re-evaluations switched off, to
+// price them
+#ifdef SIT_EXP_NO_KNIFE
+constexpr bool kKnife = false;
+#else
+constexpr bool kKnife = true;
+#endif
 
 // --------------------------------------------------------------------------------------
 // IEEE float64 (round to nearest, no contraction, no reassociation) for knife-edge decisions.
@@ -390,9 +397,14 @@ struct Ship {
 template <typename T>
 __device__ __forceinline__ void los_exact(const ConstsX64& x, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
                                           double& ect_abs, double& q, double& sum, bool& accept) {
+  // sin / cos of the leg angle as dy / L, dx / L in IEEE float64: equal to the reference's
+  // math.sin / math.cos of math.atan2 (:110-113) within an ulp or two, so e_ct is within ~1e-12 m of
+  // the reference's on the same float32 state (decisions closer than that to the threshold are the
+  // float64 libm-ulp knife edges no other libm reproduces).  Kept free of the libm's trigonometric
+  // code: this branch sits inside the step loop, whose instruction footprint is what it costs.
   const double dx = ieee_sub(cn, pn), dy = ieee_sub(ce, pe);
-  double sa, ca;
-  sincos(atan2(dy, dx), &sa, &ca);                  // math.sin / math.cos of math.atan2 (:110-113)
+  const double len = ieee_sqrt(ieee_sq2(dx, dy));
+  const double sa = len > 0.0 ? ieee_div(dy, len) : 0.0, ca = len > 0.0 ? ieee_div(dx, len) : 1.0;
   double ect = ieee_add(ieee_mul(-ieee_sub(n, pn), sa), ieee_mul(ieee_sub(e, pe), ca));
   ect_abs = fabs(ect);
   const double r2 = ieee_mul(x.los_r, x.los_r);
@@ -427,8 +439,8 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, const Const
     // knife edges of the clamp (|e| = lookahead), of the navigation-failure threshold (|e| =
     // e_tolerance) and of the anti-windup limit: float32 carries ~1e-3 m of rounding in e and
     // ~3e-4 in the integral, so inside these bands the decisions are re-taken in float64
-    const bool knife = xmin(xabs(ect_abs - c.los_r), xabs(ect_abs - c.e_tol)) < T(0.05) ||
-                       xabs(xabs(sum) - c.windup) < T(0.02);
+    const bool knife = kKnife && (xmin(xabs(ect_abs - c.los_r), xabs(ect_abs - c.e_tol)) < T(0.05) ||
+                                  xabs(xabs(sum) - c.windup) < T(0.02));
     if (knife) {
       double ex, qd, sd;
       los_exact(x, s.n, s.e, pn, pe, rt.cn, rt.ce, s.ect_int, ex, qd, sd, accept);
@@ -500,6 +512,7 @@ template <typename T>
 __device__ __forceinline__ bool rpm_fails(const Consts<T>& c, const ConstsX64& x, T w, T rpm) {
   if constexpr (kIsF32<T>) {
     // at or beyond the threshold's float32 band: decided in float64 (rare: a failing shaft)
+    if (!kKnife) return xabs(rpm) > c.rpm_max;
     if (xabs(rpm) > c.rpm_max - T(0.01)) return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > x.rpm_max;
     return false;
   } else {
@@ -513,7 +526,7 @@ template <typename T>
 __device__ __forceinline__ bool within_radius(T n0, T e0, T n1, T e1, T r, const double& r_x) {
   if constexpr (kIsF32<T>) {
     const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de, r2 = r * r;
-    if (xabs(d2 - r2) > T(1e-4) * r2) return d2 <= r2;
+    if (!kKnife || xabs(d2 - r2) > T(1e-4) * r2) return d2 <= r2;
   }
   return ieee_sqrt(ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1))) <= r_x;
 }
@@ -521,7 +534,7 @@ template <typename T>
 __device__ __forceinline__ bool closer_than(T n0, T e0, T n1, T e1, T r2, const double& r_x) {
   if constexpr (kIsF32<T>) {
     const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de;
-    if (xabs(d2 - r2) > T(1e-4) * r2) return d2 < r2;
+    if (!kKnife || xabs(d2 - r2) > T(1e-4) * r2) return d2 < r2;
   }
   return ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1)) < ieee_mul(r_x, r_x);
 }
@@ -819,6 +832,20 @@ __device__ __forceinline__ int fine_class(const Consts<T>& c, const Map<T>& m, T
   return fine_lookup(c, m, n, e, cell, word);
 }
 
+// GEOS's count over a cell's live edges in float64 at the exact point (nd, ed), starting from the
+// cell's constant parity.  Out of line: one copy serves every call site (it runs only where the
+// float32 count is unsure, or on the float64 handle), keeping the step loop's code footprint small.
+template <typename T>
+__device__ __attribute__((noinline)) bool pip_live_exact(const Edge<T>* edge, const uint8_t* live, int cnt,
+                                                         uint32_t par, double nd, double ed) {
+  uint32_t onb = 0;
+  for (int k = 0; k < cnt; ++k) {
+    const Edge<T> g = edge[live[k]];
+    count_segment(g.ax, g.ay, g.bx, g.by, ed, nd, 1u << g.poly, par, onb);
+  }
+  return (par & ~onb) != 0;
+}
+
 // float32 fast path of count_segment for a query point q known within 4e-3 m (a float32 position
 // exactly, a float32-rounded hull corner within half an ulp <= 5e-4 m inside the class grid):
 // the float32 decisions equal the exact ones unless a vertex coordinate lies within that
@@ -860,15 +887,9 @@ __device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t wor
       const Edge<T> g = m.edge[m.clive[first + k]];
       count_segment_f32(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb, unsure);
     }
-    if (!unsure) return par != 0;
+    if (!unsure || !kKnife) return par != 0;
   }
-  uint32_t par = rec.x, onb = 0;
-#pragma unroll 1
-  for (int k = 0; k < cnt; ++k) {
-    const Edge<T> g = m.edge[m.clive[first + k]];
-    count_segment(g.ax, g.ay, g.bx, g.by, ed, nd, 1u << g.poly, par, onb);
-  }
-  return (par & ~onb) != 0;
+  return pip_live_exact(m.edge, m.clive + first, cnt, rec.x, nd, ed);
 }
 
 // Polygon.contains(Point(e, n)): fine-grid class when the cell is pure (a pure cell has no
