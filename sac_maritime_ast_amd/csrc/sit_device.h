@@ -21,11 +21,11 @@ template <typename T>
 constexpr bool kIsF32 = std::is_same<T, float>::value;
 // diagnostic builds only (tools/ab2.sh): the float32 knife-edge re-evaluations switched off, to
 // price them
-#ifdef SIT_EXP_NO_KNIFE
-constexpr bool kKnife = false;
-#else
-constexpr bool kKnife = true;
+#ifndef SIT_EXP_KNIFE_MASK
+#define SIT_EXP_KNIFE_MASK 15     // 1 LOS clamp/windup, 2 shaft rpm, 4 arrival/collision radii, 8 containment
 #endif
+constexpr bool kKnifeLos = (SIT_EXP_KNIFE_MASK & 1) != 0, kKnifeRpm = (SIT_EXP_KNIFE_MASK & 2) != 0,
+               kKnifeRad = (SIT_EXP_KNIFE_MASK & 4) != 0, kKnifePip = (SIT_EXP_KNIFE_MASK & 8) != 0;
 
 // --------------------------------------------------------------------------------------
 // IEEE float64 (round to nearest, no contraction, no reassociation) for knife-edge decisions.
@@ -439,7 +439,7 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, const Const
     // knife edges of the clamp (|e| = lookahead), of the navigation-failure threshold (|e| =
     // e_tolerance) and of the anti-windup limit: float32 carries ~1e-3 m of rounding in e and
     // ~3e-4 in the integral, so inside these bands the decisions are re-taken in float64
-    const bool knife = kKnife && (xmin(xabs(ect_abs - c.los_r), xabs(ect_abs - c.e_tol)) < T(0.05) ||
+    const bool knife = kKnifeLos && (xmin(xabs(ect_abs - c.los_r), xabs(ect_abs - c.e_tol)) < T(0.05) ||
                                   xabs(xabs(sum) - c.windup) < T(0.02));
     if (knife) {
       double ex, qd, sd;
@@ -512,7 +512,7 @@ template <typename T>
 __device__ __forceinline__ bool rpm_fails(const Consts<T>& c, const ConstsX64& x, T w, T rpm) {
   if constexpr (kIsF32<T>) {
     // at or beyond the threshold's float32 band: decided in float64 (rare: a failing shaft)
-    if (!kKnife) return xabs(rpm) > c.rpm_max;
+    if (!kKnifeRpm) return xabs(rpm) > c.rpm_max;
     if (xabs(rpm) > c.rpm_max - T(0.01)) return fabs(ieee_div(ieee_mul(w, 30.0), M_PI)) > x.rpm_max;
     return false;
   } else {
@@ -526,7 +526,7 @@ template <typename T>
 __device__ __forceinline__ bool within_radius(T n0, T e0, T n1, T e1, T r, const double& r_x) {
   if constexpr (kIsF32<T>) {
     const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de, r2 = r * r;
-    if (!kKnife || xabs(d2 - r2) > T(1e-4) * r2) return d2 <= r2;
+    if (!kKnifeRad || xabs(d2 - r2) > T(1e-4) * r2) return d2 <= r2;
   }
   return ieee_sqrt(ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1))) <= r_x;
 }
@@ -534,7 +534,7 @@ template <typename T>
 __device__ __forceinline__ bool closer_than(T n0, T e0, T n1, T e1, T r2, const double& r_x) {
   if constexpr (kIsF32<T>) {
     const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de;
-    if (!kKnife || xabs(d2 - r2) > T(1e-4) * r2) return d2 < r2;
+    if (!kKnifeRad || xabs(d2 - r2) > T(1e-4) * r2) return d2 < r2;
   }
   return ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1)) < ieee_mul(r_x, r_x);
 }
@@ -887,7 +887,7 @@ __device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t wor
       const Edge<T> g = m.edge[m.clive[first + k]];
       count_segment_f32(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb, unsure);
     }
-    if (!unsure || !kKnife) return par != 0;
+    if (!unsure || !kKnifePip) return par != 0;
   }
   return pip_live_exact(m.edge, m.clive + first, cnt, rec.x, nd, ed);
 }
