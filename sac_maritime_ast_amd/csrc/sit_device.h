@@ -160,6 +160,8 @@ struct Consts {
   T bias_scale, bias_max, bias_rudder;
   // reward / termination (MSRL_env_ex.py)
   T e_tol, arrival_radius, rpm_max, min_dist2, theta, blackout_kw, rpm_k, half_len;
+  double arrive_d2_le;   // largest double x with sqrt(x) <= arrival_radius (MSRL_env_ex.py:754, 829)
+  double coll_d2;        // minimum_ship_distance ** 2 (MSRL_env_ex.py:592)
   T inv_dt, inv_e_tol, inv_maxn, inv_jp, inv_r_me, inv_r_hsg;
   T min_n, max_n, min_e, max_e;
   T pi6;
@@ -395,8 +397,8 @@ struct Ship {
 // LOS_guidance.py:110-120 in the reference's float64 arithmetic from the (float32) state: the
 // cross-track error |e|, the (clamped) e / Delta and whether the integrator accepts it
 template <typename T>
-__device__ __forceinline__ void los_exact(const ConstsX64& x, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
-                                          double& ect_abs, double& q, double& sum, bool& accept) {
+__device__ __attribute__((noinline)) void los_exact(const ConstsX64& x, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
+                                                    double& ect_abs, double& q, double& sum, bool& accept) {
   // sin / cos of the leg angle as dy / L, dx / L in IEEE float64: equal to the reference's
   // math.sin / math.cos of math.atan2 (:110-113) within an ulp or two, so e_ct is within ~1e-12 m of
   // the reference's on the same float32 state (decisions closer than that to the threshold are the
@@ -522,21 +524,25 @@ __device__ __forceinline__ bool rpm_fails(const Consts<T>& c, const ConstsX64& x
 
 // sqrt(dn^2 + de^2) <= r (arrival, MSRL_env_ex.py:754, 829) / dn^2 + de^2 < r^2 (collision, :592)
 // as the reference evaluates them in float64, decided in float32 away from the boundary
+// Both evaluated in IEEE float64 every step, branch-free (a rare-path branch inside the step loop
+// measured ~100 cycles per wave-step; these are ~10 VALU, and a float64 VALU instruction issues as
+// fast as a float32 one at one wave per SIMD).  sqrt(d2) <= r is decided as d2 <= d2_le with d2_le
+// the largest double whose correctly rounded square root is <= r (host-computed, exact).
 template <typename T>
-__device__ __forceinline__ bool within_radius(T n0, T e0, T n1, T e1, T r, const double& r_x) {
-  if constexpr (kIsF32<T>) {
-    const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de, r2 = r * r;
-    if (!kKnifeRad || xabs(d2 - r2) > T(1e-4) * r2) return d2 <= r2;
+__device__ __forceinline__ bool within_radius(T n0, T e0, T n1, T e1, double d2_le) {
+  if constexpr (!kKnifeRad && kIsF32<T>) {
+    const T dn = n0 - n1, de = e0 - e1;
+    return dn * dn + de * de <= (T)d2_le;
   }
-  return ieee_sqrt(ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1))) <= r_x;
+  return ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1)) <= d2_le;
 }
 template <typename T>
-__device__ __forceinline__ bool closer_than(T n0, T e0, T n1, T e1, T r2, const double& r_x) {
-  if constexpr (kIsF32<T>) {
-    const T dn = n0 - n1, de = e0 - e1, d2 = dn * dn + de * de;
-    if (!kKnifeRad || xabs(d2 - r2) > T(1e-4) * r2) return d2 < r2;
+__device__ __forceinline__ bool closer_than(T n0, T e0, T n1, T e1, double r2) {
+  if constexpr (!kKnifeRad && kIsF32<T>) {
+    const T dn = n0 - n1, de = e0 - e1;
+    return dn * dn + de * de < (T)r2;
   }
-  return ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1)) < ieee_mul(r_x, r_x);
+  return ieee_sq2(ieee_sub(n0, n1), ieee_sub(e0, e1)) < r2;
 }
 
 // One row of ShipModelAST.store_simulation_data (ship_model.py:645-684) from the pre-integration

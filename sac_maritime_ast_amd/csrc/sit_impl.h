@@ -643,7 +643,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
 #ifdef SIT_DIAG_PATHS
       diag_lane(c, map, s.n, s.e, dobst, type == 1, iwn, iwe, dv);
 #endif
-      const bool arrive = within_radius(s.n, s.e, rt.end_n, rt.end_e, c.arrival_radius, cs.x.arrival);
+      const bool arrive = within_radius(s.n, s.e, rt.end_n, rt.end_e, c.arrive_d2_le);
       const bool horizon = outside(c, s.n, s.e, c.half_len);
       int stop = s.stop;
       bool done = false;
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     }
     if (live) {
       const T dn = x.n[0][lane] - x.n[1][lane], de = x.e[0][lane] - x.e[1][lane];
-      const bool coll = closer_than(x.n[0][lane], x.e[0][lane], x.n[1][lane], x.e[1][lane], c.min_dist2, cs.x.min_dist);
+      const bool coll = closer_than(x.n[0][lane], x.e[0][lane], x.n[1][lane], x.e[1][lane], c.coll_d2);
       const uint32_t bt = x.bits[0][lane], bo = x.bits[1][lane];
       env_done = ((bt | bo) & kDoneBit) || coll;
       if (coll) s.stop = 1;
@@ -1144,6 +1144,14 @@ Consts<T> make_consts(const sit_handle* h) {
   c.arrival_radius = (T)p.arrival_radius;
   c.rpm_max = (T)p.shaft_rpm_max;
   c.min_dist2 = (T)(p.minimum_ship_distance * p.minimum_ship_distance);
+  c.coll_d2 = p.minimum_ship_distance * p.minimum_ship_distance;
+  {  // sqrt(x) <= r  <=>  x <= d2_le (IEEE sqrt is correctly rounded and monotone)
+    const double r = p.arrival_radius;
+    double v = r * r;
+    while (std::sqrt(std::nextafter(v, INFINITY)) <= r) v = std::nextafter(v, INFINITY);
+    while (v > 0 && std::sqrt(v) > r) v = std::nextafter(v, -INFINITY);
+    c.arrive_d2_le = v;
+  }
   c.theta = (T)p.theta;
   c.blackout_kw = (T)(me / 1000);
   c.rpm_k = (T)(30.0 / M_PI);
