@@ -693,8 +693,9 @@ __device__ __forceinline__ int orientation(T p1x, T p1y, T p2x, T p2y, T qx, T q
 // the reference's integer map) are promoted, and the query point is the caller's exact float64
 // point (a hull corner n +- l/2 of a float32 position is exact in float64, not in float32), so the
 // float32 handle decides containment exactly as the reference does for the same point.
-__device__ __forceinline__ void count_segment(double p1x, double p1y, double p2x, double p2y, double qx, double qy,
-                                              uint32_t bit, uint32_t& parity, uint32_t& onb) {
+template <typename Q>
+__device__ __forceinline__ void count_segment(Q p1x, Q p1y, Q p2x, Q p2y, Q qx, Q qy, uint32_t bit, uint32_t& parity,
+                                              uint32_t& onb) {
 #pragma clang fp reassociate(off) contract(off)
   // GEOS order: strictly-left segments and the end vertex are resolved first, horizontal
   // segments never count, straddling segments count when the point is to their left
@@ -724,7 +725,7 @@ __device__ bool point_in_polys(const Map<T>& m, double qn, double qe) {
     if (qx < bb[0] || qx > bb[1] || qy < bb[2] || qy > bb[3]) continue;
     for (int i = m.off[p]; i < m.off[p + 1]; ++i) {
       const Edge<T> g = m.edge[i];
-      count_segment(g.ax, g.ay, g.bx, g.by, qx, qy, 1u << g.poly, par, onb);
+      count_segment<double>(g.ax, g.ay, g.bx, g.by, qx, qy, 1u << g.poly, par, onb);
     }
   }
   return (par & ~onb) != 0;
@@ -795,8 +796,8 @@ __device__ int pip_pair_indexed(const Consts<T>& c, const Map<T>& m, double n, d
   for (int k = k0; k < k1; ++k) {
     const Edge<T> g = m.edge[m.idx[k]];
     const uint32_t bit = 1u << g.poly;
-    count_segment(g.ax, g.ay, g.bx, g.by, x0, n, bit, par0, onb0);
-    count_segment(g.ax, g.ay, g.bx, g.by, x1, n, bit, par1, onb1);
+    count_segment<double>(g.ax, g.ay, g.bx, g.by, x0, n, bit, par0, onb0);
+    count_segment<double>(g.ax, g.ay, g.bx, g.by, x1, n, bit, par1, onb1);
   }
   return ((par0 & ~onb0) != 0 ? 1 : 0) | ((par1 & ~onb1) != 0 ? 2 : 0);
 }
@@ -812,7 +813,7 @@ __device__ bool pip_indexed(const Consts<T>& c, const Map<T>& m, double n, doubl
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
     const Edge<T> g = m.edge[m.idx[k]];
-    count_segment(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
+    count_segment<double>(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
   }
   return (par & ~onb) != 0;
 }
@@ -847,7 +848,7 @@ __device__ __attribute__((noinline)) bool pip_live_exact(const Edge<T>* edge, co
   uint32_t onb = 0;
   for (int k = 0; k < cnt; ++k) {
     const Edge<T> g = edge[live[k]];
-    count_segment(g.ax, g.ay, g.bx, g.by, ed, nd, 1u << g.poly, par, onb);
+    count_segment<double>(g.ax, g.ay, g.bx, g.by, ed, nd, 1u << g.poly, par, onb);
   }
   return (par & ~onb) != 0;
 }
@@ -875,27 +876,44 @@ __device__ __forceinline__ void count_segment_f32(float p1x, float p1y, float p2
   (void)onb;
 }
 
+// how pip_cell may count in float32 (float32 handle; the float64 handle always counts in float64)
+constexpr int kPipFar = 0;     // exact point farther than the hull diagonal + 1 m from every boundary:
+                               // float32 comparisons are exact and every straddling edge's crossing is
+                               // >= 57 m away, far outside the float32 orientation error
+constexpr int kPipNear = 1;    // float32-rounded hull corner near the shore: float32 count with an
+                               // unsure flag, float64 re-count where it is raised
+constexpr int kPipExact = 2;   // no distance known (the IW point, probes): float64 count
+
 // Polygon.contains(Point(e, n)) for a point in mixed class cell `cell` (class word `word`):
 // the cell's constant crossing parity plus GEOS's count over the cell's live edges only.  (nd, ed)
-// is the exact float64 point; (n, e) its value in T.  float32: the count runs in float32 and is
-// re-run in float64 only where count_segment_f32 is unsure.
-template <typename T>
+// is the exact float64 point; (n, e) its value in T.
+template <int MODE, typename T>
 __device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t word, T n, T e, double nd, double ed) {
   const uint32_t mixed = (word >> 1) & 0x55555555u;
   const int r = m.frank[cell >> 4] + __popc(mixed & ((1u << ((cell & 15) * 2)) - 1u));
   const uint2 rec = m.crec[r];
   const int first = (int)(rec.y & 0xffffu), cnt = (int)(rec.y >> 16);
-  if constexpr (kIsF32<T>) {
+  if constexpr (kIsF32<T> && MODE == kPipFar) {
     uint32_t par = rec.x, onb = 0;
-    bool unsure = false;
 #pragma unroll 1
     for (int k = 0; k < cnt; ++k) {
       const Edge<T> g = m.edge[m.clive[first + k]];
-      count_segment_f32(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb, unsure);
+      count_segment<float>(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
     }
-    if (!unsure || !kKnifePip) return par != 0;
+    return (par & ~onb) != 0;
+  } else {
+    if constexpr (kIsF32<T> && MODE == kPipNear) {
+      uint32_t par = rec.x, onb = 0;
+      bool unsure = false;
+#pragma unroll 1
+      for (int k = 0; k < cnt; ++k) {
+        const Edge<T> g = m.edge[m.clive[first + k]];
+        count_segment_f32(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb, unsure);
+      }
+      if (!unsure || !kKnifePip) return par != 0;
+    }
+    return pip_live_exact(m.edge, m.clive + first, cnt, rec.x, nd, ed);
   }
-  return pip_live_exact(m.edge, m.clive + first, cnt, rec.x, nd, ed);
 }
 
 // Polygon.contains(Point(e, n)): fine-grid class when the cell is pure (a pure cell has no
@@ -907,7 +925,18 @@ __device__ bool pip_point(const Consts<T>& c, const Map<T>& m, T n, T e) {
   uint32_t word;
   const int cls = fine_lookup(c, m, n, e, cell, word);
   if (cls < 2) return cls == 1;
-  if (m.use_cells) return pip_cell(m, cell, word, n, e, (double)n, (double)e);
+  if (m.use_cells) return pip_cell<kPipExact>(m, cell, word, n, e, (double)n, (double)e);
+  return pip_indexed(c, m, n, e);
+}
+
+// the same for a point farther than hull_safe from every boundary (float32 count is exact there)
+template <typename T>
+__device__ bool pip_point_far(const Consts<T>& c, const Map<T>& m, T n, T e) {
+  int cell;
+  uint32_t word;
+  const int cls = fine_lookup(c, m, n, e, cell, word);
+  if (cls < 2) return cls == 1;
+  if (m.use_cells) return pip_cell<kPipFar>(m, cell, word, n, e, (double)n, (double)e);
   return pip_indexed(c, m, n, e);
 }
 
@@ -921,7 +950,7 @@ __device__ bool hull_corners(const Consts<T>& c, const Map<T>& m, T n, T e);
 
 template <typename T>
 __device__ bool hull_in_terrain(const Consts<T>& c, const Map<T>& m, T n, T e, T dobst) {
-  if (dobst > c.hull_safe) return pip_point(c, m, n, e);
+  if (dobst > c.hull_safe) return pip_point_far(c, m, n, e);
   return hull_corners(c, m, n, e);
 }
 
@@ -932,7 +961,7 @@ __device__ __forceinline__ bool hull_in_terrain_cls(const Consts<T>& c, const Ma
                                                     int cls, int cell, uint32_t word) {
   if (dobst > c.hull_safe) {
     if (cls < 2) return cls == 1;
-    if (m.use_cells) return pip_cell(m, cell, word, n, e, (double)n, (double)e);
+    if (m.use_cells) return pip_cell<kPipFar>(m, cell, word, n, e, (double)n, (double)e);
     return pip_indexed(c, m, n, e);
   }
   return hull_corners(c, m, n, e);
@@ -954,10 +983,10 @@ __device__ bool hull_corners(const Consts<T>& c, const Map<T>& m, T n, T e) {
     const int c10 = fine_lookup(c, m, nh, el, l10, w10), c11 = fine_lookup(c, m, nh, eh, l11, w11);
     if (c00 == 1 || c01 == 1 || c10 == 1 || c11 == 1) return true;
     bool hit = false;
-    if (c00 == 2) hit |= pip_cell(m, l00, w00, nl, el, ieee_sub(n, hx), ieee_sub(e, hx));
-    if (c01 == 2) hit |= pip_cell(m, l01, w01, nl, eh, ieee_sub(n, hx), ieee_add(e, hx));
-    if (c10 == 2) hit |= pip_cell(m, l10, w10, nh, el, ieee_add(n, hx), ieee_sub(e, hx));
-    if (c11 == 2) hit |= pip_cell(m, l11, w11, nh, eh, ieee_add(n, hx), ieee_add(e, hx));
+    if (c00 == 2) hit |= pip_cell<kPipNear>(m, l00, w00, nl, el, ieee_sub(n, hx), ieee_sub(e, hx));
+    if (c01 == 2) hit |= pip_cell<kPipNear>(m, l01, w01, nl, eh, ieee_sub(n, hx), ieee_add(e, hx));
+    if (c10 == 2) hit |= pip_cell<kPipNear>(m, l10, w10, nh, el, ieee_add(n, hx), ieee_sub(e, hx));
+    if (c11 == 2) hit |= pip_cell<kPipNear>(m, l11, w11, nh, eh, ieee_add(n, hx), ieee_add(e, hx));
     return hit;
   }
   const double nlo = ieee_sub(n, hx), nhi = ieee_add(n, hx), elo = ieee_sub(e, hx), ehi = ieee_add(e, hx);
