@@ -383,10 +383,11 @@ __device__ __forceinline__ void iw_point(double n, double e, double ab_len, doub
 constexpr int kExplicit = 0, kSynth = 1, kPolicy = 2;
 constexpr uint32_t kSampGeBit = 1u << 28;   // exchange-only: obstacle sampling distance >= AB_len
 
-template <typename T, int MODE, bool LDSMAP, bool LOG>
-__global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ Xchg<T> xs[2];
+// One wave's K steps: TYPE 0 steps the ships under test, TYPE 1 the obstacle ships.  The ship type
+// is a compile-time constant of each wave's loop (k_env_steps branches once, wave-uniformly, into
+// one of the two instantiations), so neither loop carries the other type's registers or branches.
+template <typename T, int MODE, bool LDSMAP, bool LOG, int TYPE>
+__device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem, Xchg<T>* xs, Consts<T>& cs) {
 #ifdef SIT_DIAG_PHASES
   const unsigned long long w_t0 = __builtin_amdgcn_s_memtime();
   const unsigned long long w_r0 = __builtin_amdgcn_s_memrealtime();
@@ -396,7 +397,6 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   // kernel-argument constants compete for the 102 SGPRs and spill to VGPR lanes (v_readlane
   // in the loop), and reading the LDS block inside the loop put ~40 dependent LDS reads on
   // each step's critical path (the register copy measured 12% faster).
-  __shared__ Consts<T> cs;
   for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
     reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
   __syncthreads();
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   // ~1.75x slower at the same occupancy-limited grid.
   const Map<T> map = LDSMAP ? stage_map(a, smem) : a.map;
   const int lane = threadIdx.x & (kWave - 1);
-  const int type = threadIdx.x >> 6;             // wave-uniform
+  constexpr int type = TYPE;
   const int n_env = a.n_env;
   const int env = blockIdx.x * kEnvsPerBlock + lane;
   const bool act = lane < kEnvsPerBlock && env < n_env;
@@ -880,6 +880,15 @@ __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
     }
   }
 #endif
+}
+
+template <typename T, int MODE, bool LDSMAP, bool LOG>
+__global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ Xchg<T> xs[2];
+  __shared__ Consts<T> cs;
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) env_steps<T, MODE, LDSMAP, LOG, 0>(a, smem, xs, cs);
+  else env_steps<T, MODE, LDSMAP, LOG, 1>(a, smem, xs, cs);
 }
 
 // MultiShipRLEnv.init_step for masked envs (one thread per ship)
