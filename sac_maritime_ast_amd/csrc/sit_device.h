@@ -207,19 +207,16 @@ constexpr int kIdxHead = kBandBase + kBands + 1;
 constexpr int kFine = 256;
 constexpr int kFineWords = kFine * kFine / 16;
 
-// Edge records hold only the end points (16 B in float32: a 16-lane ds_read_b128 group reading
-// distinct edges conflicts only for ids 16 apart, against 8 apart for the 32-B record with 1/L^2
-// and the polygon id inline); 1/L^2 and the polygon id are parallel arrays.
 template <typename T>
 struct alignas(16) Edge {
   T ax, ay, bx, by;
+  T il2;            // 1 / |edge|^2 (0 for a degenerate edge)
+  uint32_t poly;    // polygon id
 };
 
 template <typename T>
 struct Map {
   const Edge<T>* edge;      // [n_edge] (LDS copy in the step kernel)
-  const T* il2;             // [n_edge] 1 / |edge|^2 (0 for a degenerate edge)
-  const uint8_t* poly;      // [n_edge] polygon id
   const uint16_t* idx;      // packed index (LDS copy in the step kernel)
   const uint32_t* fine;     // [kFineWords] 2-bit cell classes (LDS copy in the step kernel)
   int32_t n_edge;
@@ -728,7 +725,7 @@ __device__ bool point_in_polys(const Map<T>& m, double qn, double qe) {
     if (qx < bb[0] || qx > bb[1] || qy < bb[2] || qy > bb[3]) continue;
     for (int i = m.off[p]; i < m.off[p + 1]; ++i) {
       const Edge<T> g = m.edge[i];
-      count_segment<double>(g.ax, g.ay, g.bx, g.by, qx, qy, 1u << m.poly[i], par, onb);
+      count_segment<double>(g.ax, g.ay, g.bx, g.by, qx, qy, 1u << g.poly, par, onb);
     }
   }
   return (par & ~onb) != 0;
@@ -736,24 +733,24 @@ __device__ bool point_in_polys(const Map<T>& m, double qn, double qe) {
 
 // squared distance from p to edge g (GEOS Distance::pointToSegment, squared form)
 template <typename T>
-__device__ __forceinline__ T edge_dist2(const Edge<T>& g, T il2, T px, T py) {
+__device__ __forceinline__ T edge_dist2(const Edge<T>& g, T px, T py) {
   const T ex = g.bx - g.ax, ey = g.by - g.ay;
   const T qx = px - g.ax, qy = py - g.ay;
   const T t = qx * ex + qy * ey;
   const T rx = px - g.bx, ry = py - g.by;
   const T cr = qy * ex - qx * ey;
-  const T d_a = qx * qx + qy * qy, d_b = rx * rx + ry * ry, d_s = cr * cr * il2;
+  const T d_a = qx * qx + qy * qy, d_b = rx * rx + ry * ry, d_s = cr * cr * g.il2;
   // branch-free selection (all three are cheap): keeps the edge loads of a candidate group
   // independent, so they issue back to back instead of one LDS round trip per candidate
-  const T d_bs = (t * il2 >= T(1)) ? d_b : d_s;
-  return ((il2 == T(0)) | (t <= T(0))) ? d_a : d_bs;
+  const T d_bs = (t * g.il2 >= T(1)) ? d_b : d_s;
+  return ((g.il2 == T(0)) | (t <= T(0))) ? d_a : d_bs;
 }
 
 // min over polygons of exterior.distance(Point(e, n)), full scan
 template <typename T>
 __device__ T distance_to_polys(const Map<T>& m, T n, T e) {
   T best = T(3.0e38);
-  for (int i = 0; i < m.n_edge; ++i) best = xmin(best, edge_dist2(m.edge[i], m.il2[i], e, n));
+  for (int i = 0; i < m.n_edge; ++i) best = xmin(best, edge_dist2(m.edge[i], e, n));
   return xsqrt(best);
 }
 
@@ -769,17 +766,17 @@ __device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   uint2 q = reinterpret_cast<const uint2*>(m.idx)[cell];
   const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (q.y >> 16);
   const int ng = (int)((q.y >> 8) & 0xffu);
-  auto ed2 = [&](uint32_t id) { return edge_dist2(m.edge[id], m.il2[id], e, n); };
-  T best = xmin(xmin(xmin(ed2(q.x & 0xffu), ed2((q.x >> 8) & 0xffu)), xmin(ed2((q.x >> 16) & 0xffu), ed2(q.x >> 24))),
-                ed2(q.y & 0xffu));
+  T best = xmin(xmin(xmin(edge_dist2(m.edge[q.x & 0xffu], e, n), edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n)),
+                     xmin(edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n), edge_dist2(m.edge[q.x >> 24], e, n))),
+                edge_dist2(m.edge[q.y & 0xffu], e, n));
 #pragma unroll 1
   for (int g = 0; g < ng; ++g) {
     q = grp[g];
-    const T d0 = ed2(q.x & 0xffu);
-    const T d1 = ed2((q.x >> 8) & 0xffu);
-    const T d2 = ed2((q.x >> 16) & 0xffu);
-    const T d3 = ed2(q.x >> 24);
-    const T d4 = ed2(q.y & 0xffu);
+    const T d0 = edge_dist2(m.edge[q.x & 0xffu], e, n);
+    const T d1 = edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n);
+    const T d2 = edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n);
+    const T d3 = edge_dist2(m.edge[q.x >> 24], e, n);
+    const T d4 = edge_dist2(m.edge[q.y & 0xffu], e, n);
     best = xmin(best, xmin(xmin(xmin(d0, d1), xmin(d2, d3)), d4));
   }
   return xsqrt(best);
@@ -797,9 +794,8 @@ __device__ int pip_pair_indexed(const Consts<T>& c, const Map<T>& m, double n, d
   const int k0 = m.idx[kBandBase + b], k1 = m.idx[kBandBase + b + 1];
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
-    const int id = m.idx[k];
-    const Edge<T> g = m.edge[id];
-    const uint32_t bit = 1u << m.poly[id];
+    const Edge<T> g = m.edge[m.idx[k]];
+    const uint32_t bit = 1u << g.poly;
     count_segment<double>(g.ax, g.ay, g.bx, g.by, x0, n, bit, par0, onb0);
     count_segment<double>(g.ax, g.ay, g.bx, g.by, x1, n, bit, par1, onb1);
   }
@@ -816,9 +812,8 @@ __device__ bool pip_indexed(const Consts<T>& c, const Map<T>& m, double n, doubl
   const int k0 = m.idx[kBandBase + b], k1 = m.idx[kBandBase + b + 1];
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
-    const int id = m.idx[k];
-    const Edge<T> g = m.edge[id];
-    count_segment<double>(g.ax, g.ay, g.bx, g.by, e, n, 1u << m.poly[id], par, onb);
+    const Edge<T> g = m.edge[m.idx[k]];
+    count_segment<double>(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
   }
   return (par & ~onb) != 0;
 }
@@ -848,13 +843,12 @@ __device__ __forceinline__ int fine_class(const Consts<T>& c, const Map<T>& m, T
 // cell's constant parity.  Out of line: one copy serves every call site (it runs only where the
 // float32 count is unsure, or on the float64 handle), keeping the step loop's code footprint small.
 template <typename T>
-__device__ __attribute__((noinline)) bool pip_live_exact(const Edge<T>* edge, const uint8_t* poly, const uint8_t* live,
-                                                         int cnt, uint32_t par, double nd, double ed) {
+__device__ __attribute__((noinline)) bool pip_live_exact(const Edge<T>* edge, const uint8_t* live, int cnt,
+                                                         uint32_t par, double nd, double ed) {
   uint32_t onb = 0;
   for (int k = 0; k < cnt; ++k) {
-    const int id = live[k];
-    const Edge<T> g = edge[id];
-    count_segment<double>(g.ax, g.ay, g.bx, g.by, ed, nd, 1u << poly[id], par, onb);
+    const Edge<T> g = edge[live[k]];
+    count_segment<double>(g.ax, g.ay, g.bx, g.by, ed, nd, 1u << g.poly, par, onb);
   }
   return (par & ~onb) != 0;
 }
@@ -903,9 +897,8 @@ __device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t wor
     uint32_t par = rec.x, onb = 0;
 #pragma unroll 1
     for (int k = 0; k < cnt; ++k) {
-      const int id = m.clive[first + k];
-      const Edge<T> g = m.edge[id];
-      count_segment<float>(g.ax, g.ay, g.bx, g.by, e, n, 1u << m.poly[id], par, onb);
+      const Edge<T> g = m.edge[m.clive[first + k]];
+      count_segment<float>(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
     }
     return (par & ~onb) != 0;
   } else {
@@ -914,13 +907,12 @@ __device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t wor
       bool unsure = false;
 #pragma unroll 1
       for (int k = 0; k < cnt; ++k) {
-        const int id = m.clive[first + k];
-        const Edge<T> g = m.edge[id];
-        count_segment_f32(g.ax, g.ay, g.bx, g.by, e, n, 1u << m.poly[id], par, onb, unsure);
+        const Edge<T> g = m.edge[m.clive[first + k]];
+        count_segment_f32(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb, unsure);
       }
       if (!unsure || !kKnifePip) return par != 0;
     }
-    return pip_live_exact(m.edge, m.poly, m.clive + first, cnt, rec.x, nd, ed);
+    return pip_live_exact(m.edge, m.clive + first, cnt, rec.x, nd, ed);
   }
 }
 

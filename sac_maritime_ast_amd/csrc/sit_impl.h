@@ -163,8 +163,6 @@ __device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* ds
                                      (__attribute__((address_space(3))) void*)(dst + 16 * (i - lane)), 16, 0, 0);
   Map<T> m = a.map;
   m.edge = reinterpret_cast<const Edge<T>*>(dst);
-  m.il2 = reinterpret_cast<const T*>(dst + (reinterpret_cast<const unsigned char*>(a.map.il2) - src));
-  m.poly = reinterpret_cast<const uint8_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.poly) - src));
   m.idx = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.idx) - src));
   m.fine = reinterpret_cast<const uint32_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.fine) - src));
   m.frank = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.frank) - src));
@@ -1046,7 +1044,7 @@ struct sit_handle {
   // map
   unsigned char* map = nullptr;
   int n_poly = 0, n_vert = 0;
-  size_t map_il2 = 0, map_poly = 0, map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0, map_frank = 0, map_crec = 0, map_clive = 0;
+  size_t map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0, map_frank = 0, map_crec = 0, map_clive = 0;
   int use_cells = 0;
   int64_t n_mixed = 0, n_live = 0;
   int lds_attr[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
@@ -1230,8 +1228,6 @@ KArgs<T> make_args(const sit_handle* h) {
   a.map.n_edge = h->n_vert;
   a.map.use_index = h->use_index;
   a.map.edge = reinterpret_cast<const Edge<T>*>(h->map);
-  a.map.il2 = reinterpret_cast<const T*>(h->map + h->map_il2);
-  a.map.poly = reinterpret_cast<const uint8_t*>(h->map + h->map_poly);
   a.map.idx = reinterpret_cast<const uint16_t*>(h->map + h->map_idx);
   a.map.fine = reinterpret_cast<const uint32_t*>(h->map + h->map_fine);
   a.map.frank = reinterpret_cast<const uint16_t*>(h->map + h->map_frank);

@@ -459,12 +459,9 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     std::copy(bentries.begin(), bentries.end(), idx.begin() + head);
     std::copy(grest.begin(), grest.end(), idx.begin() + gbase);
   }
-  // blob: [Edge<T>[nv]][1/L^2 T[nv]][poly u8[nv]][u16 index][u32 classes] (staged into LDS)
-  //       [ring offsets][bboxes] (fallback, global)
+  // blob: [Edge<T>[nv]][u16 index][u32 classes] (staged into LDS) [ring offsets][bboxes] (fallback, global)
   const size_t esz = rs == 8 ? sizeof(Edge<double>) : sizeof(Edge<float>);
-  size_t o = (nv * esz + 15) & ~size_t(15);
-  h->map_il2 = o; o = (o + nv * rs + 15) & ~size_t(15);
-  h->map_poly = o; o = align256(o + nv);
+  size_t o = align256(nv * esz);
   h->map_idx = o; o = align256(o + idx.size() * 2);
   h->map_fine = o; o = align256(o + fine.size() * 4);
   h->use_cells = cells_ok ? 1 : 0;
@@ -479,15 +476,12 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
   std::vector<unsigned char> host(o, 0);
   for (int e = 0; e < nv; ++e) {
     if (rs == 8) {
-      Edge<double> g{vx[e], vy[e], bxv[e], byv[e]};
+      Edge<double> g{vx[e], vy[e], bxv[e], byv[e], il2[e], (uint32_t)poly_of[e]};
       std::memcpy(host.data() + e * esz, &g, sizeof(g));
-      reinterpret_cast<double*>(host.data() + h->map_il2)[e] = il2[e];
     } else {
-      Edge<float> g{(float)vx[e], (float)vy[e], (float)bxv[e], (float)byv[e]};
+      Edge<float> g{(float)vx[e], (float)vy[e], (float)bxv[e], (float)byv[e], (float)il2[e], (uint32_t)poly_of[e]};
       std::memcpy(host.data() + e * esz, &g, sizeof(g));
-      reinterpret_cast<float*>(host.data() + h->map_il2)[e] = (float)il2[e];
     }
-    host[h->map_poly + e] = (unsigned char)poly_of[e];
   }
   std::memcpy(host.data() + h->map_idx, idx.data(), idx.size() * 2);
   std::memcpy(host.data() + h->map_fine, fine.data(), fine.size() * 4);
