@@ -731,24 +731,18 @@ __device__ bool point_in_polys(const Map<T>& m, double qn, double qe) {
   return (par & ~onb) != 0;
 }
 
-// squared distance from p to edge g, for minimisation over a closed ring's edges (GEOS
-// Distance::pointToSegment: the distance to the line when the projection parameter
-// r = (p - A).(B - A) / |B - A|^2 lies in (0, 1), else the distance to the nearer end point).
-// Each edge contributes min(|p - A|^2, the line distance if r in (0, 1)): its far end point B is the
-// start point A of the ring's next edge, which is also a nearest edge wherever B is nearest, so
-// the minimum over a candidate list is unchanged (the index keeps every edge that attains the
-// minimum somewhere in its cell; sit_load_map).  The line distance is the cross product's (an
-// error of order eps |p - A|, against eps |B - A| for the clamped-projection form).  Branch-free,
-// so a candidate group's edge loads issue back to back.
+// squared distance from p to edge g (GEOS Distance::pointToSegment: the end point's distance when
+// the projection parameter r = (p - A).(B - A) / |B - A|^2 falls outside (0, 1), else the distance
+// to the line), as the distance to the point A + clamp(r, 0, 1) (B - A): the same value up to
+// rounding, in ~12 VALU instead of ~19 (no three-way select; a degenerate edge has il2 = 0, so
+// r = 0 and the end point A).  Branch-free, so a candidate group's edge loads issue back to back.
 template <typename T>
 __device__ __forceinline__ T edge_dist2(const Edge<T>& g, T px, T py) {
   const T ex = g.bx - g.ax, ey = g.by - g.ay;
   const T qx = px - g.ax, qy = py - g.ay;
-  const T t = qx * ex + qy * ey;
-  const T cr = qy * ex - qx * ey;
-  const T d_a = qx * qx + qy * qy;
-  const T d_s = ((t > T(0)) & (t * g.il2 < T(1))) ? cr * cr * g.il2 : d_a;
-  return xmin(d_a, d_s);
+  const T r = xmin(xmax((qx * ex + qy * ey) * g.il2, T(0)), T(1));
+  const T dx = qx - r * ex, dy = qy - r * ey;
+  return dx * dx + dy * dy;
 }
 
 // min over polygons of exterior.distance(Point(e, n)), full scan
