@@ -731,18 +731,19 @@ __device__ bool point_in_polys(const Map<T>& m, double qn, double qe) {
   return (par & ~onb) != 0;
 }
 
-// squared distance from p to edge g (GEOS Distance::pointToSegment: the end point's distance when
-// the projection parameter r = (p - A).(B - A) / |B - A|^2 falls outside (0, 1), else the distance
-// to the line), as the distance to the point A + clamp(r, 0, 1) (B - A): the same value up to
-// rounding, in ~12 VALU instead of ~19 (no three-way select; a degenerate edge has il2 = 0, so
-// r = 0 and the end point A).  Branch-free, so a candidate group's edge loads issue back to back.
+// squared distance from p to edge g (GEOS Distance::pointToSegment, squared form)
 template <typename T>
 __device__ __forceinline__ T edge_dist2(const Edge<T>& g, T px, T py) {
   const T ex = g.bx - g.ax, ey = g.by - g.ay;
   const T qx = px - g.ax, qy = py - g.ay;
-  const T r = xmin(xmax((qx * ex + qy * ey) * g.il2, T(0)), T(1));
-  const T dx = qx - r * ex, dy = qy - r * ey;
-  return dx * dx + dy * dy;
+  const T t = qx * ex + qy * ey;
+  const T rx = px - g.bx, ry = py - g.by;
+  const T cr = qy * ex - qx * ey;
+  const T d_a = qx * qx + qy * qy, d_b = rx * rx + ry * ry, d_s = cr * cr * g.il2;
+  // branch-free selection (all three are cheap): keeps the edge loads of a candidate group
+  // independent, so they issue back to back instead of one LDS round trip per candidate
+  const T d_bs = (t * g.il2 >= T(1)) ? d_b : d_s;
+  return ((g.il2 == T(0)) | (t <= T(0))) ? d_a : d_bs;
 }
 
 // min over polygons of exterior.distance(Point(e, n)), full scan
