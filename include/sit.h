@@ -62,6 +62,12 @@ extern "C" {
 #define SIT_SG_GEN 1   /* 'GEN'   (PTO)  */
 #define SIT_SG_OFF 2   /* anything else  */
 
+/* ---- machinery model (sit_params.machinery_model) ---------------------------------- */
+#define SIT_MACH_SHAFT 0      /* ShipMachineryModel: shaft speed ODE, thrust = k D^4 w|w| (ship_engine.py:298-395) */
+#define SIT_MACH_SIMPLIFIED 1 /* SimplifiedMachineryModel: first-order thrust-force lag (ship_engine.py:398-433)
+                               * with ThrottleFromSpeedSetPointSimplifiedPropulsion (controllers.py:154-172);
+                               * the shaft_speed state holds the thrust force [N], see sit_params */
+
 /* ---- status bitmask: one bit per reference status string, in the order the
  *      reference concatenates them (MSRL_env_ex.py:755-803, 830-874, 897-899) ------- */
 #define SIT_ST_TEST_ENDPOINT (1u << 0)   /* "|Test ship reaches endpoint|"             */
@@ -156,7 +162,7 @@ typedef struct sit_params {
   double main_engine_capacity;   /* MachineryModeParams of the operating mode */
   double electrical_capacity;
   int32_t shaft_generator_state; /* SIT_SG_* */
-  int32_t _pad0;
+  int32_t machinery_model;       /* SIT_MACH_* (0 = the reference's ShipModelAST machinery)  */
   double rated_speed_main_engine_rpm;
   double linear_friction_main_engine;
   double linear_friction_hybrid_shaft_generator;
@@ -199,6 +205,13 @@ typedef struct sit_params {
    * 162-163): logging only (trajectory log, fuel keys) */
   double fuel_me_a, fuel_me_b, fuel_me_c;
   double fuel_dg_a, fuel_dg_b, fuel_dg_c;
+  /* SIT_MACH_SIMPLIFIED only (SimplifiedPropulsionMachinerySystemConfiguration, ship_engine.py:
+   * 148-157): thrust_force_dynamic_time_constant [s].  In that mode the ship-speed PI gains
+   * kp_ship_speed / ki_ship_speed are ThrottleFromSpeedSetPointSimplifiedPropulsion's kp / ki
+   * (throttle saturated to [0, 1.1]), the shaft-speed PI is unused, the shaft_speed state and
+   * SIT_INIT_SHAFT_SPEED hold the thrust force [N] (initial_thrust_force), and the observed shaft
+   * speed is 0 (the model has no shaft, so no mechanical failure). */
+  double thrust_force_dynamic_time_constant;
 } sit_params;
 
 /* Fill `p` with the configuration of test_beds/test_policy.py:94-226 (PTI mode). */

@@ -31,6 +31,7 @@ import numpy as np
 # configuration: the reference's NamedTuple values (test_beds/test_policy.py:94-226)
 # ------------------------------------------------------------------------------------
 SG_MOTOR, SG_GEN, SG_OFF = 0, 1, 2
+MACH_SHAFT, MACH_SIMPLIFIED = 0, 1
 
 DEFAULT_PARAMS = dict(
     # ShipConfiguration (test_policy.py:102-118)
@@ -87,6 +88,11 @@ DEFAULT_PARAMS = dict(
     # Baudouin 6M26.3 diesel generators; ship_engine.py:89-115)
     fuel_me_a=128.9, fuel_me_b=-168.9, fuel_me_c=246.8,
     fuel_dg_a=108.7, fuel_dg_b=-289.9, fuel_dg_c=324.9,
+    # machinery model: ShipMachineryModel (the reference's ShipModelAST) or SimplifiedMachineryModel
+    # (ship_engine.py:398-433, with ThrottleFromSpeedSetPointSimplifiedPropulsion, controllers.py:
+    # 154-172, whose kp / ki are kp_ship_speed / ki_ship_speed); the reference configures no time
+    # constant for it, 30 s is this library's default
+    machinery_model=MACH_SHAFT, thrust_force_dynamic_time_constant=30.0,
 )
 
 # ShipModelAST.store_simulation_data keys, in order (ship_model.py:645-684)
@@ -151,6 +157,10 @@ def derive(p: dict) -> dict:
     c["rudder_max"] = p["max_rudder_angle_degrees"] * np.pi / 180           # ship_engine.py:203
     c["bias_rudder"] = float(np.deg2rad(p["bias_rudder_degrees"]))           # MSRL_Env.py:250
     c["thrust_coeff"] = p["propeller_diameter"] ** 4 * p["propeller_speed_to_thrust_force_coefficient"]
+    # SimplifiedMachineryModel (ship_engine.py:420-428)
+    c["simplified"] = p.get("machinery_model", MACH_SHAFT) == MACH_SIMPLIFIED
+    c["p_simpl"] = avail_me + avail_el
+    c["k_thrust"] = 2160 / 790
     return c
 
 
@@ -439,14 +449,19 @@ class OracleEnvs:
         s["fuel"][t] = np.where(m, s["fuel"][t] + (rate_me + rate_el) * dt, s["fuel"][t])
         w = pre["shaft_speed"]
         torque = np.minimum(thr * c["avail_me"] / (w + 0.1), c["avail_me"] / 5 * np.pi / 30)   # ship_engine.py:369-376
+        thrust = c["thrust_coeff"] * w * np.abs(w)
+        if c["simplified"]:
+            # no reference row (store_simulation_data reads the shaft speed, which the simplified
+            # model lacks): shaft speed and torque 0, thrust force from the thrust state
+            torque, thrust = np.zeros_like(w), w
         row = np.stack([
             s["ticks"][t] * dt, pre["north"], pre["east"], pre["yaw"] * 180 / np.pi, rudder * 180 / np.pi,
-            pre["surge"], pre["sway"], pre["yaw_rate"] * 180 / np.pi, w * 30 / np.pi, lp_me, lp_el,
+            pre["surge"], pre["sway"], pre["yaw_rate"] * 180 / np.pi, self._rpm(w), lp_me, lp_el,
             load_me / 1000, np.full_like(thr, c["main_engine_capacity"] / 1000), load_el / 1000,
             np.full_like(thr, c["electrical_capacity"] / 1000), (load_el + load_me) / 1000,
             (thr * c["avail_prop"]) / 1000, rate_me, rate_el, rate_me + rate_el,
             s["fuel_me"][t], s["fuel_el"][t], s["fuel"][t], torque,
-            c["thrust_coeff"] * w * np.abs(w) / 1000, ect,
+            thrust / 1000, ect,
             np.abs(pre["yaw"] - psi_ref)])                          # get_heading_error: radians (label says deg)
         return row
 
@@ -463,6 +478,11 @@ class OracleEnvs:
         if "wpt_north" in st:
             self.tab_n = np.asarray(st["wpt_north"], dtype=np.float64).copy()
             self.tab_e = np.asarray(st["wpt_east"], dtype=np.float64).copy()
+
+    def _rpm(self, w):
+        """Observed shaft speed omega * 30 / pi (ship_model.py:652); SimplifiedMachineryModel has no
+        shaft (its state slot holds the thrust force): 0."""
+        return np.zeros_like(w) if self.c["simplified"] else w * 30 / np.pi
 
     def _wpt(self, t, idx):
         ar = np.arange(self.n_env)
@@ -508,9 +528,14 @@ class OracleEnvs:
         e1 = self.init[t, INIT_FIELDS.index("desired_speed")] - u
         i1 = s["ship_speed_i"][t] + e1 * dt
         w_des = e1 * c["kp_ship_speed"] + i1 * c["ki_ship_speed"]
-        e2 = w_des - u
-        i2 = s["shaft_speed_i"][t] + e2 * dt
-        thr = e2 * c["kp_shaft_speed"] + i2 * c["ki_shaft_speed"]
+        if c["simplified"]:
+            # ThrottleFromSpeedSetPointSimplifiedPropulsion.throttle (controllers.py:170-172)
+            i2 = s["shaft_speed_i"][t]
+            thr = np.maximum(0.0, np.minimum(w_des, 1.1))
+        else:
+            e2 = w_des - u
+            i2 = s["shaft_speed_i"][t] + e2 * dt
+            thr = e2 * c["kp_shaft_speed"] + i2 * c["ki_shaft_speed"]
         if trace is not None:
             trace["heading_ref"] = psi_ref
         s["next_wpt"][t] = np.where(m, k, s["next_wpt"][t])
@@ -546,14 +571,20 @@ class OracleEnvs:
         d_n = cps * u - sps * v
         d_e = sps * u + cps * v
         d_psi = r
-        # ShipMachineryModel.update_shaft_equation (ship_engine.py:355-395)
-        tq_me = np.minimum(thr * c["avail_me"] / (w + 0.1), c["avail_me"] / 5 * np.pi / 30)
-        tq_hsg = np.minimum(thr * c["avail_el"] / (w + 0.1), c["avail_el"] / 5 * np.pi / 30)
-        eq_me = (tq_me - c["linear_friction_main_engine"] * w) / c["gear_ratio_between_main_engine_and_propeller"]
-        eq_hsg = (tq_hsg - c["linear_friction_hybrid_shaft_generator"] * w) / \
-            c["gear_ratio_between_hybrid_shaft_generator_and_propeller"]
-        d_w = (eq_me + eq_hsg - c["propeller_speed_to_torque_coefficient"] * w ** 2) / c["propeller_inertia"]
-        thrust = c["thrust_coeff"] * w * np.abs(w)                           # ship_engine.py:363-366
+        if c["simplified"]:
+            # SimplifiedMachineryModel.update_thrust_force (ship_engine.py:423-428); w is the thrust
+            power = thr * c["p_simpl"]
+            d_w = (-c["k_thrust"] * w + power) / c["thrust_force_dynamic_time_constant"]
+            thrust = w
+        else:
+            # ShipMachineryModel.update_shaft_equation (ship_engine.py:355-395)
+            tq_me = np.minimum(thr * c["avail_me"] / (w + 0.1), c["avail_me"] / 5 * np.pi / 30)
+            tq_hsg = np.minimum(thr * c["avail_el"] / (w + 0.1), c["avail_el"] / 5 * np.pi / 30)
+            eq_me = (tq_me - c["linear_friction_main_engine"] * w) / c["gear_ratio_between_main_engine_and_propeller"]
+            eq_hsg = (tq_hsg - c["linear_friction_hybrid_shaft_generator"] * w) / \
+                c["gear_ratio_between_hybrid_shaft_generator_and_propeller"]
+            d_w = (eq_me + eq_hsg - c["propeller_speed_to_torque_coefficient"] * w ** 2) / c["propeller_inertia"]
+            thrust = c["thrust_coeff"] * w * np.abs(w)                       # ship_engine.py:363-366
         # ShipModelAST.three_dof_kinetics (ship_model.py:576-606)
         vcn, vce = c["current_velocity_component_from_north"], c["current_velocity_component_from_east"]
         vc_u = cps * vcn + sps * vce              # inv(rotation()) . vel_c
@@ -615,7 +646,7 @@ class OracleEnvs:
         if bias:
             thr = np.clip(thr * c["bias_throttle_scale"], 0.0, c["bias_throttle_max"])
             rudder = np.clip(rudder + c["bias_rudder"], -c["rudder_max"], c["rudder_max"])
-        rpm = s["shaft_speed"][t] * 30 / np.pi
+        rpm = self._rpm(s["shaft_speed"][t])
         pme = self._power_me_kw(thr)
         s["last_rpm"][t], s["last_e_ct"][t], s["last_power_me"][t] = rpm, ect, pme
         pre = {k: s[k][t].copy() for k in ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed")}
@@ -666,7 +697,7 @@ class OracleEnvs:
         if c["collision_bias"]:  # is_collision_imminent on the all-zero next_states: always True (Q1)
             thr = np.clip(thr * c["bias_throttle_scale"], 0.0, c["bias_throttle_max"])
             rudder = np.clip(rudder + c["bias_rudder"], -c["rudder_max"], c["rudder_max"])
-        rpm0 = s["shaft_speed"][0] * 30 / np.pi
+        rpm0 = self._rpm(s["shaft_speed"][0])
         pme0 = self._power_me_kw(thr)
         s["last_rpm"][0], s["last_e_ct"][0], s["last_power_me"][0] = rpm0, ect0, pme0
         if self.log is not None:       # store_simulation_data before update/integrate (:256-260)
@@ -702,7 +733,7 @@ class OracleEnvs:
             last[0] = s["ticks"][1] * c["integration_step"]
             log1 = np.where(run[None, :], row1, last)
             s["last_log"] = log1
-        rpm1 = s["shaft_speed"][1] * 30 / np.pi
+        rpm1 = self._rpm(s["shaft_speed"][1])
         pme1 = self._power_me_kw(thr1)
         s["last_rpm"][1] = np.where(run, rpm1, s["last_rpm"][1])
         s["last_e_ct"][1] = np.where(run, ect1, s["last_e_ct"][1])

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("SIT_LIBRARY", os.path.join(HERE, "libsit.so"))
 SIT_OK, SIT_E_INVALID, SIT_E_HIP, SIT_E_NOMEM, SIT_E_STATE = 0, -1, -2, -3, -4
 SIT_F32, SIT_F64 = 32, 64
 SIT_SG_MOTOR, SIT_SG_GEN, SIT_SG_OFF = 0, 1, 2
+SIT_MACH_SHAFT, SIT_MACH_SIMPLIFIED = 0, 1
 SIT_DT_REAL, SIT_DT_I32, SIT_DT_U32 = 0, 1, 2
 SIT_OBS_DIM = 10
 SIT_TRANSITION_DIM = 24
@@ -43,7 +44,7 @@ PARAM_FIELDS = [
     ("rho_air", _D), ("front_height", _D), ("side_height", _D), ("cx", _D), ("cy", _D), ("cn", _D),
     ("integration_step", _D),
     ("hotel_load", _D), ("main_engine_capacity", _D), ("electrical_capacity", _D),
-    ("shaft_generator_state", c_int32), ("_pad0", c_int32),
+    ("shaft_generator_state", c_int32), ("machinery_model", c_int32),
     ("rated_speed_main_engine_rpm", _D), ("linear_friction_main_engine", _D),
     ("linear_friction_hybrid_shaft_generator", _D), ("gear_ratio_between_main_engine_and_propeller", _D),
     ("gear_ratio_between_hybrid_shaft_generator_and_propeller", _D), ("propeller_inertia", _D),
@@ -58,7 +59,7 @@ PARAM_FIELDS = [
     ("e_tolerance", _D), ("arrival_radius", _D), ("shaft_rpm_max", _D), ("minimum_ship_distance", _D),
     ("bias_throttle_scale", _D), ("bias_throttle_max", _D), ("bias_rudder_degrees", _D),
     ("fuel_me_a", _D), ("fuel_me_b", _D), ("fuel_me_c", _D), ("fuel_dg_a", _D), ("fuel_dg_b", _D),
-    ("fuel_dg_c", _D),
+    ("fuel_dg_c", _D), ("thrust_force_dynamic_time_constant", _D),
 ]
 
 

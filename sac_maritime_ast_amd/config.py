@@ -27,7 +27,13 @@ def params(**overrides) -> _lib.SitParams:
 def params_from_reference(ship_config=None, environment_config=None, simulation_config=None,
                           machinery_config=None, throttle_gains=None, heading_gains=None,
                           los_parameters=None, args=None, **overrides) -> _lib.SitParams:
-    """sit_params from reference-style configuration objects (duck-typed NamedTuples)."""
+    """sit_params from reference-style configuration objects (duck-typed NamedTuples).
+
+    A ``SimplifiedPropulsionMachinerySystemConfiguration`` (ship_engine.py:148-157; recognised by its
+    thrust_force_dynamic_time_constant) selects SIT_MACH_SIMPLIFIED; ``throttle_gains`` may then be
+    the kp / ki of ThrottleFromSpeedSetPointSimplifiedPropulsion (controllers.py:160-169), which
+    become kp_ship_speed / ki_ship_speed.
+    """
     p = params()
     if ship_config is not None:
         for f in ("dead_weight_tonnage", "coefficient_of_deadweight_to_displacement", "bunkers", "ballast",
@@ -56,7 +62,11 @@ def params_from_reference(ship_config=None, environment_config=None, simulation_
                   "propeller_speed_to_torque_coefficient", "propeller_diameter",
                   "propeller_speed_to_thrust_force_coefficient", "rudder_angle_to_sway_force_coefficient",
                   "rudder_angle_to_yaw_force_coefficient", "max_rudder_angle_degrees"):
-            setattr(p, f, float(getattr(mc, f)))
+            if hasattr(mc, f):      # the simplified configuration has no shaft fields
+                setattr(p, f, float(getattr(mc, f)))
+        if hasattr(mc, "thrust_force_dynamic_time_constant"):
+            p.machinery_model = _lib.SIT_MACH_SIMPLIFIED
+            p.thrust_force_dynamic_time_constant = float(mc.thrust_force_dynamic_time_constant)
         modes = getattr(mc.machinery_modes, "list_of_modes", mc.machinery_modes)
         mode = modes[int(mc.machinery_operating_mode)]
         p.main_engine_capacity = float(mode.main_engine_capacity)
@@ -70,8 +80,11 @@ def params_from_reference(ship_config=None, environment_config=None, simulation_
                 setattr(p, f"fuel_{tag}_b", float(co.b))
                 setattr(p, f"fuel_{tag}_c", float(co.c))
     if throttle_gains is not None:
-        for f in ("kp_ship_speed", "ki_ship_speed", "kp_shaft_speed", "ki_shaft_speed"):
-            setattr(p, f, float(getattr(throttle_gains, f)))
+        if hasattr(throttle_gains, "kp_ship_speed"):
+            for f in ("kp_ship_speed", "ki_ship_speed", "kp_shaft_speed", "ki_shaft_speed"):
+                setattr(p, f, float(getattr(throttle_gains, f)))
+        else:                       # (kp, ki) of the simplified-propulsion throttle
+            p.kp_ship_speed, p.ki_ship_speed = float(throttle_gains.kp), float(throttle_gains.ki)
     if heading_gains is not None:
         p.heading_kp, p.heading_kd, p.heading_ki = (float(heading_gains.kp), float(heading_gains.kd),
                                                     float(heading_gains.ki))

@@ -151,6 +151,10 @@ struct Consts {
   T me_cap, hotel, load_el_gen;
   int32_t sg_mode;
   int32_t collision_bias;
+  // SimplifiedMachineryModel (ship_engine.py:398-433; SIT_MACH_SIMPLIFIED): the shaft-speed slot
+  // `w` holds the thrust force, d_thrust = (p_simpl * throttle - k_thrust * thrust) / tau
+  int32_t mach_simpl;
+  T k_thrust, inv_tau, p_simpl;
   // controllers
   T kp1, ki1, kp2, ki2, kp_h, kd_h, ki_h;
   // LOS
@@ -174,6 +178,14 @@ struct Consts {
   T el_cap, fuel_me_a, fuel_me_b, fuel_me_c, fuel_dg_a, fuel_dg_b, fuel_dg_c, rad2deg;
   ConstsX64 x;
 };
+
+// machinery model of a handle: a compile-time constant inside the step kernel (MACH = 0 shaft,
+// 1 simplified; k_env_steps dispatches once per wave), read from the constants elsewhere (-1)
+template <int MACH, typename T>
+__device__ __forceinline__ bool simpl_of(const Consts<T>& c) {
+  if constexpr (MACH >= 0) return MACH == 1;
+  else return c.mach_simpl != 0;
+}
 
 // island map (obstacle.py:92-124): edge i of the closed rings runs from (ax, ay) to (bx, by);
 // coordinates are (x = east, y = north) as in obstacle.py:128.  One Edge record per edge (one
@@ -418,7 +430,7 @@ __device__ __attribute__((noinline)) void los_exact(const ConstsX64& x, T n, T e
 
 // ect_over: |e_ct| > e_tolerance (the navigation-failure predicate, MSRL_env_ex.py:560-576) decided
 // exactly (float64 inside the float32 band)
-template <typename T>
+template <typename T, int MACH = -1>
 __device__ __forceinline__ void guidance_control(const Consts<T>& c, const ConstsX64& x, Ship<T>& s, Route<T>& rt,
                                                  T v_des, T& rudder, T& thr, T& ect_abs, T& psi_ref_out,
                                                  bool& ect_over) {
@@ -478,22 +490,33 @@ __device__ __forceinline__ void guidance_control(const Consts<T>& c, const Const
   const T e1 = v_des - s.u;
   s.i1 = s.i1 + e1 * c.dt;
   const T wdes = e1 * c.kp1 + s.i1 * c.ki1;
-  const T e2 = wdes - s.u;
-  s.i2 = s.i2 + e2 * c.dt;
-  thr = e2 * c.kp2 + s.i2 * c.ki2;
+  if (simpl_of<MACH>(c)) {
+    // ThrottleFromSpeedSetPointSimplifiedPropulsion.throttle (controllers.py:170-172): the ship-speed
+    // PI alone, saturated to [0, 1.1]
+    thr = xclip(wdes, T(0), T(1.1));
+  } else {
+    const T e2 = wdes - s.u;
+    s.i2 = s.i2 + e2 * c.dt;
+    thr = e2 * c.kp2 + s.i2 * c.ki2;
+  }
 }
 
 // EngineThrottleFromSpeedSetPoint.throttle (controllers.py:52-62, 138-143) in the reference's
 // float64 arithmetic from the pre-step integrals i1, i2 and surge u; with the collision bias of
 // MSRL_Env.py:244-251 when `bias`
 template <typename T>
-__device__ __forceinline__ double throttle_exact(const ConstsX64& x, T u, T v_des, T i1, T i2, bool bias) {
+__device__ __forceinline__ double throttle_exact(const ConstsX64& x, T u, T v_des, T i1, T i2, bool bias, bool simpl) {
   const double e1 = ieee_sub(v_des, u);
   const double ii1 = ieee_add(i1, ieee_mul(e1, x.dt));
   const double wdes = ieee_dot2(e1, x.kp1, ii1, x.ki1);
-  const double e2 = ieee_sub(wdes, u);
-  const double ii2 = ieee_add(i2, ieee_mul(e2, x.dt));
-  double thr = ieee_dot2(e2, x.kp2, ii2, x.ki2);
+  double thr;
+  if (simpl) {   // ThrottleFromSpeedSetPointSimplifiedPropulsion (controllers.py:170-172)
+    thr = fmax(0.0, fmin(wdes, 1.1));
+  } else {
+    const double e2 = ieee_sub(wdes, u);
+    const double ii2 = ieee_add(i2, ieee_mul(e2, x.dt));
+    thr = ieee_dot2(e2, x.kp2, ii2, x.ki2);
+  }
   if (bias) thr = fmax(0.0, fmin(ieee_mul(thr, x.bias_scale), x.bias_max));
   return thr;
 }
@@ -510,8 +533,9 @@ __device__ __forceinline__ double power_me_kw_exact(int sg_mode, const ConstsX64
 
 // is_mechanical_failure (MSRL_env_ex.py:554-558): |shaft speed * 30 / pi| > shaft_rpm_max, with
 // rpm = w * 30 / pi (ship_model.py:652) re-taken in float64 near the threshold
-template <typename T>
+template <typename T, int MACH = -1>
 __device__ __forceinline__ bool rpm_fails(const Consts<T>& c, const ConstsX64& x, T w, T rpm) {
+  if (simpl_of<MACH>(c)) return false;   // no shaft: the observed shaft speed is 0
   if constexpr (kIsF32<T>) {
     // at or beyond the threshold's float32 band: decided in float64 (rare: a failing shaft)
     if (!kKnifeRpm) return xabs(rpm) > c.rpm_max;
@@ -550,7 +574,7 @@ __device__ __forceinline__ bool closer_than(T n0, T e0, T n1, T e1, double r2) {
 // (BaseMachineryModel.fuel_consumption, ship_engine.py:263-289; load split
 // MachineryMode.distribute_load, ship_engine.py:46-76; torque :369-376; thrust :363-366).
 // (An out-of-line version made the whole step kernel 2.2x slower: calls give it a stack.)
-template <typename T>
+template <typename T, int MACH = -1>
 __device__ __forceinline__ void store_log_row(const Consts<T>& c, T* dst, size_t stride, const Ship<T>& s, T thr,
                                               T rudder, T ect, T psi_ref, T& fuel_me, T& fuel_el, T& fuel) {
   const T total = thr * c.avail_prop;
@@ -583,8 +607,8 @@ __device__ __forceinline__ void store_log_row(const Consts<T>& c, T* dst, size_t
       T(s.ticks) * c.dt, s.n, s.e, s.psi * c.rad2deg, rudder * c.rad2deg, s.u, s.v, s.r * c.rad2deg,
       w * c.rpm_k, lp_me, lp_el, load_me / T(1000), c.me_cap / T(1000), load_el / T(1000),
       c.el_cap / T(1000), (load_el + load_me) / T(1000), total / T(1000), rate_me, rate_el, rate_me + rate_el,
-      fuel_me, fuel_el, fuel, xmin(thr * c.avail_me / (w + T(0.1)), c.tqcap_me),
-      c.thrust_k * w * xabs(w) / T(1000), ect, xabs(s.psi - psi_ref)};
+      fuel_me, fuel_el, fuel, simpl_of<MACH>(c) ? T(0) : xmin(thr * c.avail_me / (w + T(0.1)), c.tqcap_me),
+      (simpl_of<MACH>(c) ? w : c.thrust_k * w * xabs(w)) / T(1000), ect, xabs(s.psi - psi_ref)};
 #pragma unroll
   for (int k = 0; k < SIT_LOG_KEYS; ++k) dst[k * stride] = v[k];
 }
@@ -602,18 +626,25 @@ __device__ __forceinline__ T power_me_kw(const Consts<T>& c, T thr) {
 
 // update_differentials + integrate_differentials; sp, cp = sin/cos of the pre-step heading
 // (computed by the caller at the start of the step, off the guidance dependency chain) (ship_model.py:624-643, ship_engine.py:355-395)
-template <typename T>
+template <typename T, int MACH = -1>
 __device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T thr, T rudder, T sp, T cp) {
   const T u = s.u, v = s.v, r = s.r, w = s.w;
   // kinematics: eta_dot = R(psi) nu
   const T d_n = cp * u - sp * v;
   const T d_e = sp * u + cp * v;
-  // shaft equation with pre-step omega
-  const T inv_w = T(1) / (w + T(0.1));
-  const T tq_me = xmin(thr * c.avail_me * inv_w, c.tqcap_me);
-  const T tq_hsg = xmin(thr * c.avail_el * inv_w, c.tqcap_el);
-  const T d_w = ((tq_me - c.d_me * w) * c.inv_r_me + (tq_hsg - c.d_hsg * w) * c.inv_r_hsg - c.kp_prop * (w * w)) * c.inv_jp;
-  const T thrust = c.thrust_k * w * xabs(w);
+  T d_w, thrust;
+  if (simpl_of<MACH>(c)) {
+    // SimplifiedMachineryModel.update_thrust_force (ship_engine.py:423-428): w is the thrust force
+    thrust = w;
+    d_w = (thr * c.p_simpl - c.k_thrust * w) * c.inv_tau;
+  } else {
+    // shaft equation with pre-step omega
+    const T inv_w = T(1) / (w + T(0.1));
+    const T tq_me = xmin(thr * c.avail_me * inv_w, c.tqcap_me);
+    const T tq_hsg = xmin(thr * c.avail_el * inv_w, c.tqcap_el);
+    d_w = ((tq_me - c.d_me * w) * c.inv_r_me + (tq_hsg - c.d_hsg * w) * c.inv_r_hsg - c.kp_prop * (w * w)) * c.inv_jp;
+    thrust = c.thrust_k * w * xabs(w);
+  }
   // current in body frame: R(psi)^T v_c
   const T vc_u = cp * c.vc_n + sp * c.vc_e;
   const T vc_v = -sp * c.vc_n + cp * c.vc_e;

@@ -386,7 +386,7 @@ constexpr uint32_t kSampGeBit = 1u << 28;   // exchange-only: obstacle sampling 
 // One wave's K steps: TYPE 0 steps the ships under test, TYPE 1 the obstacle ships.  The ship type
 // is a compile-time constant of each wave's loop (k_env_steps branches once, wave-uniformly, into
 // one of the two instantiations), so neither loop carries the other type's registers or branches.
-template <typename T, int MODE, bool LDSMAP, bool LOG, int TYPE>
+template <typename T, int MODE, bool LDSMAP, bool LOG, int TYPE, int MACH>
 __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem, Xchg<T>* xs, Consts<T>& cs) {
 #ifdef SIT_DIAG_PHASES
   const unsigned long long w_t0 = __builtin_amdgcn_s_memtime();
@@ -578,15 +578,15 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
           }
           const T pre_n = s.n, pre_e = s.e;
           T rudder, thr, psi_ref;
-          guidance_control(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+          guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
           o_rpm = s.w * c.rpm_k;
           o_pme = power_me_kw(c, thr);
           s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
           if (p_lg) {
-            store_log_row(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
+            store_log_row<T, MACH>(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
             for (int kk = 0; kk < SIT_LOG_KEYS; ++kk) a.st.last_log[kk * row_step + env] = p_lg[kk * row_step];
           }
-          ship_dynamics(c, s, thr, rudder, sp, cp);
+          ship_dynamics<T, MACH>(c, s, thr, rudder, sp, cp);
           if (!init_f) {                 // distance between the last two stored positions
             const T dn = pre_n - ppn, de = pre_e - ppe;
             const T d = xsqrt(dn * dn + de * de);
@@ -600,7 +600,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
         const T i1_0 = s.i1, i2_0 = s.i2;   // pre-step integrals (blackout knife edge)
-        guidance_control(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+        guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
         if (c.collision_bias) {          // is_collision_imminent() on all-zero states (Q1)
           thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
           rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
@@ -609,17 +609,18 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         o_pme = power_me_kw(c, thr);
         // failure predicates on pre-integration values (MSRL_env_ex.py:554-558, 578-582), exact:
         // float64 where the float32 margin is inside the float32 band (always for the float64 handle)
-        mech = rpm_fails(c, cs.x, s.w, o_rpm);
+        mech = rpm_fails<T, MACH>(c, cs.x, s.w, o_rpm);
         // MOTOR (PTI): load_me = min(total, ME capacity) <= ME capacity, so no blackout ever (Q7)
         if (c.sg_mode != SIT_SG_MOTOR) {
           blk = o_pme > c.blackout_kw;
           if (!kIsF32<T> || xabs(o_pme - c.blackout_kw) <= T(1e-4) * (xabs(o_pme) + T(1)))
             blk = power_me_kw_exact(c.sg_mode, cs.x, throttle_exact(cs.x, s.u, v_des, i1_0, i2_0,
-                                                                    c.collision_bias != 0)) > cs.x.blackout;
+                                                                    c.collision_bias != 0, MACH == 1))
+                  > cs.x.blackout;
         }
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
-        if (p_lg) store_log_row(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
-        ship_dynamics(c, s, thr, rudder, sp, cp);
+        if (p_lg) store_log_row<T, MACH>(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
+        ship_dynamics<T, MACH>(c, s, thr, rudder, sp, cp);
         s.ticks += 1;
       }
 
@@ -882,13 +883,15 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
 #endif
 }
 
-template <typename T, int MODE, bool LDSMAP, bool LOG>
+// MACH: the handle's machinery model as a kernel template argument (a runtime branch on it inside
+// the step loop measured ~4% slower: it splits the scheduling regions of guidance and dynamics)
+template <typename T, int MODE, bool LDSMAP, bool LOG, int MACH>
 __global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Xchg<T> xs[2];
   __shared__ Consts<T> cs;
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) env_steps<T, MODE, LDSMAP, LOG, 0>(a, smem, xs, cs);
-  else env_steps<T, MODE, LDSMAP, LOG, 1>(a, smem, xs, cs);
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) env_steps<T, MODE, LDSMAP, LOG, 0, MACH>(a, smem, xs, cs);
+  else env_steps<T, MODE, LDSMAP, LOG, 1, MACH>(a, smem, xs, cs);
 }
 
 // MultiShipRLEnv.init_step for masked envs (one thread per ship)
@@ -1047,7 +1050,8 @@ struct sit_handle {
   size_t map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0, map_frank = 0, map_crec = 0, map_clive = 0;
   int use_cells = 0;
   int64_t n_mixed = 0, n_live = 0;
-  int lds_attr[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
+  int lds_attr[24] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                      -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
@@ -1136,6 +1140,12 @@ Consts<T> make_consts(const sit_handle* h) {
   c.thrust_k = (T)(std::pow(p.propeller_diameter, 4.0) * p.propeller_speed_to_thrust_force_coefficient);
   c.me_cap = (T)me; c.hotel = (T)hotel; c.load_el_gen = (T)std::min(hotel, el);
   c.sg_mode = p.shaft_generator_state;
+  c.mach_simpl = p.machinery_model == SIT_MACH_SIMPLIFIED;
+  // SimplifiedMachineryModel (ship_engine.py:420-428): power = load_perc * (available propulsion
+  // power of the main engine + of the electrical side), k_thrust = 2160 / 790
+  c.k_thrust = (T)(2160.0 / 790.0);
+  c.inv_tau = (T)(1.0 / p.thrust_force_dynamic_time_constant);
+  c.p_simpl = (T)(avail_me + avail_el);
   c.collision_bias = p.collision_bias;
   c.kp1 = (T)p.kp_ship_speed; c.ki1 = (T)p.ki_ship_speed;
   c.kp2 = (T)p.kp_shaft_speed; c.ki2 = (T)p.ki_shaft_speed;
@@ -1163,7 +1173,7 @@ Consts<T> make_consts(const sit_handle* h) {
   }
   c.theta = (T)p.theta;
   c.blackout_kw = (T)(me / 1000);
-  c.rpm_k = (T)(30.0 / M_PI);
+  c.rpm_k = c.mach_simpl ? T(0) : (T)(30.0 / M_PI);   // SimplifiedMachineryModel: no shaft
   c.inv_dt = (T)(1.0 / p.integration_step);
   c.inv_e_tol = (T)(1.0 / p.e_tolerance);
   c.inv_maxn = (T)(1.0 / h->max_n);
@@ -1267,7 +1277,7 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   auto go = [&](auto kern) -> int {
     // the dynamic-LDS attribute is set once per kernel and size (not per launch: launches may be
     // captured into HIP graphs)
-    const int slot = (mode * 2 + (lds_map ? 1 : 0)) * 2 + (io.log ? 1 : 0);
+    const int slot = ((mode * 2 + (lds_map ? 1 : 0)) * 2 + (io.log ? 1 : 0)) * 2 + (a.c.mach_simpl ? 1 : 0);
     if (lds_map && h->lds_attr[slot] != (int)lds) {
       HIP_TRY(h, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       h->lds_attr[slot] = (int)lds;
@@ -1275,10 +1285,14 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(128), lds, stream, a);
     return SIT_OK;
   };
+  auto pick_mach = [&](auto mode_tag, auto mach_tag) -> int {
+    constexpr int M = decltype(mode_tag)::value, K = decltype(mach_tag)::value;
+    if (io.log) return lds_map ? go(k_env_steps<T, M, true, true, K>) : go(k_env_steps<T, M, false, true, K>);
+    return lds_map ? go(k_env_steps<T, M, true, false, K>) : go(k_env_steps<T, M, false, false, K>);
+  };
   auto pick = [&](auto mode_tag) -> int {
-    constexpr int M = decltype(mode_tag)::value;
-    if (io.log) return lds_map ? go(k_env_steps<T, M, true, true>) : go(k_env_steps<T, M, false, true>);
-    return lds_map ? go(k_env_steps<T, M, true, false>) : go(k_env_steps<T, M, false, false>);
+    if (a.c.mach_simpl) return pick_mach(mode_tag, std::integral_constant<int, 1>{});
+    return pick_mach(mode_tag, std::integral_constant<int, 0>{});
   };
   int rc;
   if (mode == kSynth) rc = pick(std::integral_constant<int, kSynth>{});

@@ -168,6 +168,10 @@ void sit_params_default(sit_params* p) {
   // SpecificFuelConsumptionWartila6L26 / Baudouin6M26Dot3 (ship_engine.py:89-115), test_policy.py:162-163
   p->fuel_me_a = 128.9; p->fuel_me_b = -168.9; p->fuel_me_c = 246.8;
   p->fuel_dg_a = 108.7; p->fuel_dg_b = -289.9; p->fuel_dg_c = 324.9;
+  // SIT_MACH_SIMPLIFIED only: the reference configures no SimplifiedMachineryModel (no value to
+  // quote); 30 s is this library's default
+  p->machinery_model = SIT_MACH_SHAFT;
+  p->thrust_force_dynamic_time_constant = 30;
 }
 
 const char* sit_last_error(const sit_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
@@ -187,6 +191,10 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
     return fail(nullptr, SIT_E_INVALID, "integration_step, sampling_frequency and lookahead_distance must be positive");
   if (p->shaft_generator_state < SIT_SG_MOTOR || p->shaft_generator_state > SIT_SG_OFF)
     return fail(nullptr, SIT_E_INVALID, "shaft_generator_state out of range");
+  if (p->machinery_model != SIT_MACH_SHAFT && p->machinery_model != SIT_MACH_SIMPLIFIED)
+    return fail(nullptr, SIT_E_INVALID, "machinery_model out of range");
+  if (p->machinery_model == SIT_MACH_SIMPLIFIED && !(p->thrust_force_dynamic_time_constant > 0))
+    return fail(nullptr, SIT_E_INVALID, "thrust_force_dynamic_time_constant must be > 0");
   sit_handle* h = new sit_handle();
   h->precision = precision;
   h->n_env = n_env;

@@ -305,6 +305,93 @@ def gen_sim_trajectory(ref, name, route, pose, n_steps, bias=False, mode="PTI"):
     return data
 
 
+# SimplifiedMachineryModel (ship_engine.py:398-433).  The reference defines it but wires it into no
+# ship model: ShipModelAST.update_differentials / store_simulation_data call the shaft model's
+# thrust() and omega, which it lacks.  The fixture composes the reference's own pieces the way
+# ShipModelAST.update_differentials composes the shaft model (ship_model.py:624-630): kinematics,
+# SimplifiedMachineryModel.update_thrust_force(throttle), three_dof_kinetics(thrust_force=its
+# thrust), integrate_differentials (which integrates the thrust); the throttle is
+# ThrottleFromSpeedSetPointSimplifiedPropulsion (controllers.py:154-172).  No trajectory log (the
+# reference's store_simulation_data cannot run with this model).
+TAU_SIMPL = 30.0
+
+
+def build_ship_simplified(ref, route, pose, thrust0, mode="PTI", kp=7.0, ki=0.13):
+    se, ctl = ref.se, ref.ctl
+    ship, _, ap = build_ship(ref, route, pose, mode=mode)
+    sg, me_cap, el_cap = MODES[mode]
+    m = se.MachineryMode(params=se.MachineryModeParams(main_engine_capacity=me_cap, electrical_capacity=el_cap,
+                                                       shaft_generator_state=sg))
+    cfg = se.SimplifiedPropulsionMachinerySystemConfiguration(
+        hotel_load=200000, machinery_modes=se.MachineryModes([m]), machinery_operating_mode=0,
+        specific_fuel_consumption_coefficients_me=se.SpecificFuelConsumptionWartila6L26().fuel_consumption_coefficients(),
+        specific_fuel_consumption_coefficients_dg=se.SpecificFuelConsumptionBaudouin6M26Dot3().fuel_consumption_coefficients(),
+        thrust_force_dynamic_time_constant=TAU_SIMPL, rudder_angle_to_sway_force_coefficient=50e3,
+        rudder_angle_to_yaw_force_coefficient=500e3, max_rudder_angle_degrees=30)
+    ship.ship_machinery_model = se.SimplifiedMachineryModel(machinery_config=cfg, time_step=DT,
+                                                            initial_thrust_force=thrust0)
+    thr = ctl.ThrottleFromSpeedSetPointSimplifiedPropulsion(kp=kp, ki=ki, time_step=DT)
+    return ship, thr, ap
+
+
+def sim_step_simplified(ship, thr, ap, v_des, bias=False):
+    rudder = ap.rudder_angle_from_sampled_route(north_position=ship.north, east_position=ship.east,
+                                                heading=ship.yaw_angle)
+    throttle = thr.throttle(speed_set_point=v_des, measured_speed=ship.forward_speed)
+    if bias:
+        throttle *= 0.5
+        throttle = np.clip(throttle, 0.0, 1.1)
+        rudder += np.deg2rad(3)
+        rudder = np.clip(rudder, -ap.heading_controller.max_rudder_angle, ap.heading_controller.max_rudder_angle)
+    mm = ship.ship_machinery_model
+    power_me = mm.mode.distribute_load(load_perc=throttle, hotel_load=mm.hotel_load).load_on_main_engine / 1000
+    thrust = mm.thrust
+    ship.three_dof_kinematics()
+    mm.update_thrust_force(throttle)
+    ship.three_dof_kinetics(thrust_force=mm.thrust, rudder_angle=rudder)
+    out = dict(rudder=float(rudder), throttle=float(throttle), heading_ref=ap.heading_ref, e_ct=ap.navigate.e_ct,
+               rpm=0.0, power_me=power_me, d_north=ship.d_north, d_east=ship.d_east, d_yaw=ship.d_yaw,
+               d_surge=ship.d_forward_speed, d_sway=ship.d_sideways_speed, d_yaw_rate=ship.d_yaw_rate,
+               d_shaft_speed=mm.d_thrust, thrust=thrust)
+    ship.integrate_differentials()
+    ship.int.next_time()
+    return out
+
+
+def snapshot_simplified(ship, thr, ap):
+    pid = ap.heading_controller.ship_heading_controller
+    return dict(north=ship.north, east=ship.east, yaw=ship.yaw_angle, surge=ship.forward_speed,
+                sway=ship.sideways_speed, yaw_rate=ship.yaw_rate, shaft_speed=ship.ship_machinery_model.thrust,
+                ship_speed_i=thr.ship_speed_controller.error_i, shaft_speed_i=0.0,
+                heading_i=pid.error_i, heading_prev=pid.prev_error, e_ct_int=ap.navigate.e_ct_int,
+                next_wpt=ap.next_wpt)
+
+
+def gen_sim_simplified(ref, name, route, pose, n_steps, thrust0, v_des, bias=False, mode="PTI"):
+    ship, thr, ap = build_ship_simplified(ref, route, pose, thrust0, mode=mode)
+    pre = {k: [] for k in SIM_FIELDS}
+    out = {k: [] for k in OUT_FIELDS}
+    for _ in range(n_steps):
+        snap = snapshot_simplified(ship, thr, ap)
+        for k in SIM_FIELDS:
+            pre[k].append(snap[k])
+        o = sim_step_simplified(ship, thr, ap, v_des, bias)
+        for k in OUT_FIELDS:
+            out[k].append(o[k])
+    snap = snapshot_simplified(ship, thr, ap)
+    r, nr = _route_arrays(route)
+    sg, me_cap, el_cap = MODES[mode]
+    data = {"route": r, "n_route": np.int64(nr), "pose": np.asarray(pose, float), "bias": np.int64(bias),
+            "mode": np.asarray([MODE_ID[sg], me_cap, el_cap], float), "simplified": np.asarray([TAU_SIMPL, 7.0, 0.13]),
+            "v_des": np.float64(v_des)}
+    for k in SIM_FIELDS:
+        data["pre_" + k] = np.asarray(pre[k] + [snap[k]], dtype=np.float64)
+    for k in OUT_FIELDS:
+        data["out_" + k] = np.asarray(out[k], dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, f"sim_{name}.npz"), **data)
+    return data
+
+
 def gen_sim_teacher_forced(ref, rng, src, n_cases=600):
     """One-step teacher-forced cases: random pre-states around recorded trajectories plus
     knife-edge constructions (waypoint acceptance circle, e_ct^2 = r^2, windup limit, throttle < 0)."""
@@ -589,8 +676,17 @@ def gen_env_cases(ref, obstacle, env_mod, seed):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seed", type=int, default=25450)
+    ap.add_argument("--only", choices=("simplified",), help="write only this group of fixtures")
     args = ap.parse_args()
     ref = _import_reference()
+    # SimplifiedMachineryModel: PTI from rest with zero thrust (throttle saturated, then regulating
+    # 3 m/s), and the collision-biased PTO variant slowing from 6 to 3.5 m/s
+    gen_sim_simplified(ref, "simpl", R_TEST, (R_TEST[0][0], R_TEST[0][1], math.atan2(4000, 300), 0, 0, 0), 3000, 0.0,
+                       3.0)
+    gen_sim_simplified(ref, "simpl_pto", R_OBS, (R_OBS[0][0], R_OBS[0][1], math.atan2(-100, 6400), 6.0, 0, 0), 800,
+                       2.0e5, 3.5, bias=True, mode="PTO")
+    if args.only == "simplified":
+        return
     # C1 / K1: route [[0,0],[10000,10000]], 1000 zero-action steps, no bias
     gen_sim_trajectory(ref, "c1", [[0.0, 0.0], [10000.0, 10000.0]], (0, 0, np.pi / 4, 0, 0, 0), 1000)
     # K2: route R_A, 600 steps

@@ -39,6 +39,9 @@ SCALE = dict(north=1e4, east=1e4, yaw=np.pi, surge=10.0, sway=10.0, yaw_rate=0.1
              rudder=np.pi, throttle=1.0, heading_ref=np.pi, e_ct=1e3, rpm=1e3, power_me=1e3,
              d_north=10.0, d_east=10.0, d_yaw=0.1, d_surge=0.1, d_sway=0.1, d_yaw_rate=1e-3,
              d_shaft_speed=1.0, thrust=1e5, reward=1.0, wpt_north=1e4, wpt_east=1e4)
+# SimplifiedMachineryModel fixtures: the shaft-speed slot holds the thrust force [N] and its rate
+# d_thrust = (power - k F) / tau [N/s] (a difference of ~1e6 N terms near equilibrium)
+SCALE_SIMPL = dict(SCALE, shaft_speed=1e5, d_shaft_speed=1e4)
 OBS_SCALE = np.array([1e4, 1e4, np.pi, 1e3, 1e3, 1e3, 1e4, 1e4, np.pi, 1e3])
 
 
@@ -72,6 +75,28 @@ def init_rows(poses, omega0=OMEGA0, v_des=8.5, pi2=114.0):
     return init
 
 
+def sim_scale(d):
+    return SCALE_SIMPL if "simplified" in d.files else SCALE
+
+
+def sim_params(d, **over):
+    """Oracle parameters of a sim_* fixture: its machinery mode, and for the SimplifiedMachineryModel
+    fixtures (key "simplified" = time constant, throttle kp, ki) that model."""
+    p = params_for(d["mode"] if "mode" in d.files else None, **over)
+    if "simplified" in d.files:
+        tau, kp, ki = (float(x) for x in d["simplified"])
+        p.update(machinery_model=so.MACH_SIMPLIFIED, thrust_force_dynamic_time_constant=tau, kp_ship_speed=kp,
+                 ki_ship_speed=ki)
+    return p
+
+
+def sim_init(d, poses):
+    """init rows for a sim_* fixture (desired speed, initial shaft speed / thrust, shaft PI integral)."""
+    if "simplified" in d.files:
+        return init_rows(poses, omega0=float(d["pre_shaft_speed"][0]), v_des=float(d["v_des"]), pi2=0.0)
+    return init_rows(poses)
+
+
 def sim_oracle(d):
     """Oracle with one env whose two ships both carry the fixture's ship."""
     route = d["route"]
@@ -79,9 +104,8 @@ def sim_oracle(d):
     routes = np.stack([route, route])[None]
     n_wpt = np.array([[nr, nr]])
     pose = d["pose"] if "pose" in d.files else np.zeros(6)
-    init = init_rows(np.stack([pose, pose])[None])
-    mode = d["mode"] if "mode" in d.files else None
-    return so.OracleEnvs(params_for(mode), routes, n_wpt, init, POLYS)
+    init = sim_init(d, np.stack([pose, pose])[None])
+    return so.OracleEnvs(sim_params(d), routes, n_wpt, init, POLYS)
 
 
 def sim_state_from(d, prefix, i, oracle):
@@ -142,9 +166,8 @@ def sim_oracle_batch(d, n_env):
     routes = np.repeat(np.stack([route, route])[None], n_env, axis=0)
     n_wpt = np.full((n_env, 2), nr)
     pose = d["pose"] if "pose" in d.files else np.zeros(6)
-    init = init_rows(np.repeat(np.stack([pose, pose])[None], n_env, axis=0))
-    mode = d["mode"] if "mode" in d.files else None
-    return so.OracleEnvs(params_for(mode), routes, n_wpt, init, POLYS)
+    init = sim_init(d, np.repeat(np.stack([pose, pose])[None], n_env, axis=0))
+    return so.OracleEnvs(sim_params(d), routes, n_wpt, init, POLYS)
 
 
 def rel_err(a, b, scale):

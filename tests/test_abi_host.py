@@ -93,6 +93,23 @@ def test_params_from_reference_style_objects():
     assert p.shaft_generator_state == _lib.SIT_SG_GEN and p.main_engine_capacity == 2160e3
     assert p.sampling_frequency == 9 and p.theta == 1.5
     assert config.shaft_speed_max(p) == pytest.approx(69.11503837897544)
+    assert p.machinery_model == _lib.SIT_MACH_SHAFT
+
+
+def test_params_from_reference_simplified_machinery():
+    """A SimplifiedPropulsionMachinerySystemConfiguration (ship_engine.py:148-157) selects the
+    SimplifiedMachineryModel; the (kp, ki) of ThrottleFromSpeedSetPointSimplifiedPropulsion
+    (controllers.py:160-169) become the ship-speed PI gains."""
+    mode = SimpleNamespace(main_engine_capacity=0.0, electrical_capacity=1020e3, shaft_generator_state="MOTOR")
+    mc = SimpleNamespace(hotel_load=200000, machinery_modes=SimpleNamespace(list_of_modes=[mode]),
+                         machinery_operating_mode=0, thrust_force_dynamic_time_constant=45.0,
+                         rudder_angle_to_sway_force_coefficient=40e3, rudder_angle_to_yaw_force_coefficient=400e3,
+                         max_rudder_angle_degrees=25)
+    p = config.params_from_reference(machinery_config=mc, throttle_gains=SimpleNamespace(kp=2.0, ki=0.05))
+    assert p.machinery_model == _lib.SIT_MACH_SIMPLIFIED and p.thrust_force_dynamic_time_constant == 45.0
+    assert p.kp_ship_speed == 2.0 and p.ki_ship_speed == 0.05
+    assert p.rudder_angle_to_sway_force_coefficient == 40e3 and p.max_rudder_angle_degrees == 25
+    assert p.propeller_inertia == config.params().propeller_inertia     # shaft fields untouched
 
 
 def test_scenario_matches_survey():

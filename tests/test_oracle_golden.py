@@ -10,32 +10,35 @@ import numpy as np
 import pytest
 
 from helpers import (OBS_SCALE, SCALE, SIM_FIELDS, env_oracle, env_state_all_rows, env_state_from,
-                     golden, golden_names, rel_err, sim_oracle, sim_oracle_batch, sim_state_all_rows,
+                     golden, golden_names, rel_err, sim_oracle, sim_oracle_batch, sim_scale, sim_state_all_rows,
                      sim_state_from)
 from oracle import sit_oracle as so
 
 TOL = 1e-11
 
 
-def _check_fields(got, want, names, tol, where):
+def _check_fields(got, want, names, tol, where, scale=SCALE):
     for k in names:
-        err = rel_err(got[k], want[k], SCALE.get(k, 1.0)).max()
+        err = rel_err(got[k], want[k], scale.get(k, 1.0)).max()
         assert err <= tol, f"{where}: field {k} rel err {err:.3e}"
 
 
-@pytest.mark.parametrize("name", ["sim_c1", "sim_k2", "sim_bias", "sim_pto", "sim_mec"])
+@pytest.mark.parametrize("name", ["sim_c1", "sim_k2", "sim_bias", "sim_pto", "sim_mec", "sim_simpl", "sim_simpl_pto"])
 def test_sim_trajectory_free_running(name):
-    """Whole trajectories of one ship (C1 = sim_c1: 1000 zero-action steps), no teacher forcing."""
+    """Whole trajectories of one ship (C1 = sim_c1: 1000 zero-action steps), no teacher forcing.
+    sim_simpl*: the SimplifiedMachineryModel (ship_engine.py:398-433) with its throttle
+    controller (controllers.py:154-172), composed as make_golden.py documents."""
     d = golden(name)
     o = sim_oracle(d)
     bias = bool(d["bias"])
+    scale = sim_scale(d)
     for i in range(len(d["out_rudder"])):
         _check_fields({k: o.s[k][1] for k in SIM_FIELDS}, {k: d["pre_" + k][i] for k in SIM_FIELDS},
-                      SIM_FIELDS, TOL, f"{name} step {i}")
+                      SIM_FIELDS, TOL, f"{name} step {i}", scale)
         out = o.sim_step(1, bias)
         for k, v in out.items():
             if "out_" + k in d.files:
-                err = rel_err(v[0], d["out_" + k][i], SCALE[k])
+                err = rel_err(v[0], d["out_" + k][i], scale[k])
                 assert err <= TOL, f"{name} step {i}: {k} rel err {err:.3e}"
 
 
@@ -147,7 +150,8 @@ def test_nominal_episode_matches_survey_k4():
 # trajectory logs: simulation_results (ship_model.py:645-700, fuel model ship_engine.py:256-292)
 # and reward_results (MSRL_env_ex.py:926-964), recorded from the reference by make_golden.py
 # ------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("name", [n for n in golden_names("sim_") if n != "sim_teacher_forced"])
+@pytest.mark.parametrize("name", [n for n in golden_names("sim_") if n != "sim_teacher_forced"
+                                  and not n.startswith("sim_simpl")])   # no reference log for that model
 def test_oracle_simulation_log_vs_reference(name):
     d = golden(name)
     o = sim_oracle(d)
