@@ -355,6 +355,24 @@ size_t sit_rollout_args_size(void);
 int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t head_stride,
                      const void* noise, const int32_t* request_env, const int32_t* request_count,
                      int32_t deterministic, void* policy_action, int32_t* policy_ready, void* stream);
+/* Policy mode helper, the whole actor in one kernel: the SAC-AST Gaussian policy's MLP
+ * (ast_core/nn_models/mlp.py:95-148: obs[SIT_OBS_DIM] -> 256 -> ReLU -> 256 -> ReLU -> (mu, log_sigma),
+ * main_ast.py:67's hidden sizes) in float32 on request rows q < min(*request_count, capacity), then the
+ * head and scatter of sit_policy_apply (GaussianPolicy.get_actions, gaussian_policy.py:114-126, as
+ * agent.select_action mode 1 calls it, main_ast.py:344-349).
+ *   weights  float32[SIT_ACTOR_WEIGHTS]: W1 [256][SIT_OBS_DIM] (torch Linear layout), b1 [256],
+ *            W2 transposed [256 in][256 out], b2 [256], W3 [2][256], b3 [2]
+ *   obs      real[capacity][SIT_OBS_DIM] (the request_obs rows of sit_rollout_args)
+ *   served   int64[1] or NULL: += min(*request_count, capacity)
+ *   blocks_done int32[1] or NULL (zero-initialised scratch): when given, *request_count is reset to 0
+ *            once every block has read it, ready for the next sit_rollout launch. */
+#define SIT_ACTOR_HIDDEN 256
+#define SIT_ACTOR_WEIGHTS (SIT_ACTOR_HIDDEN * SIT_OBS_DIM + SIT_ACTOR_HIDDEN + SIT_ACTOR_HIDDEN * SIT_ACTOR_HIDDEN + \
+                           SIT_ACTOR_HIDDEN + 2 * SIT_ACTOR_HIDDEN + 2)
+int sit_policy_actor(sit_handle* h, int32_t capacity, const float* weights, const void* obs, const void* noise,
+                     const int32_t* request_env, int32_t* request_count, int32_t deterministic,
+                     void* policy_action, int32_t* policy_ready, int64_t* served, int32_t* blocks_done,
+                     void* stream);
 
 /* ---- state export / import (device blob) ------------------------------------------ */
 /* The dynamic state of all envs (ship states, controller integrators, route tables,

@@ -19,6 +19,8 @@ SIT_MACH_SHAFT, SIT_MACH_SIMPLIFIED = 0, 1
 SIT_DT_REAL, SIT_DT_I32, SIT_DT_U32 = 0, 1, 2
 SIT_OBS_DIM = 10
 SIT_TRANSITION_DIM = 24
+SIT_ACTOR_HIDDEN = 256
+SIT_ACTOR_WEIGHTS = SIT_ACTOR_HIDDEN * SIT_OBS_DIM + SIT_ACTOR_HIDDEN + SIT_ACTOR_HIDDEN ** 2 + SIT_ACTOR_HIDDEN + 2 * SIT_ACTOR_HIDDEN + 2
 SIT_LOG_KEYS, SIT_LOG_ROWS = 27, 62
 INIT_FIELDS = ("north", "east", "yaw", "surge", "sway", "yaw_rate", "shaft_speed", "desired_speed",
                "ship_speed_i", "shaft_speed_i")
@@ -106,6 +108,8 @@ SIGNATURES = {
     "sit_map_info": (c_int32, [c_void_p, c_void_p, c_int32]),
     "sit_policy_apply": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                                    c_void_p, c_void_p, c_void_p]),
+    "sit_policy_actor": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sit_probe_map": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sit_selftest_f64": (c_int32, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "sit_restart": (c_int32, [c_void_p, c_void_p]),

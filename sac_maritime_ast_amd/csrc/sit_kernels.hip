@@ -2,6 +2,7 @@
 // Kernels and host helpers: sit_impl.h.  float32 step kernels: sit_steps_f32.hip.
 
 #include "sit_impl.h"
+#include "sit_actor.h"
 
 namespace {
 
@@ -95,6 +96,26 @@ int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t 
     hipLaunchKernelGGL(k_policy_apply<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, capacity,
                        (const float*)head, head_stride, (const float*)noise, request_env, request_count,
                        deterministic, (float*)policy_action, policy_ready, h->n_env);
+  HIP_TRY(h, hipGetLastError());
+  return SIT_OK;
+}
+
+int sit_policy_actor(sit_handle* h, int32_t capacity, const float* weights, const void* obs, const void* noise,
+                     const int32_t* request_env, int32_t* request_count, int32_t deterministic,
+                     void* policy_action, int32_t* policy_ready, int64_t* served, int32_t* blocks_done,
+                     void* stream) {
+  if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
+  if (capacity <= 0 || !weights || !obs || !request_env || !request_count || !policy_action || !policy_ready ||
+      (!deterministic && !noise))
+    return fail(h, SIT_E_INVALID, "policy_actor: bad arguments");
+  int rc = h->precision == SIT_F64
+               ? launch_policy_actor<double>(h, capacity, weights, obs, noise, request_env, request_count,
+                                             deterministic, policy_action, policy_ready, served, blocks_done,
+                                             (hipStream_t)stream)
+               : launch_policy_actor<float>(h, capacity, weights, obs, noise, request_env, request_count,
+                                            deterministic, policy_action, policy_ready, served, blocks_done,
+                                            (hipStream_t)stream);
+  if (rc) return rc;
   HIP_TRY(h, hipGetLastError());
   return SIT_OK;
 }

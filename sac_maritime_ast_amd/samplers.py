@@ -77,17 +77,49 @@ class GaussianPolicy(nn.Module):
         return action, log_pi, mu, log_sig
 
 
+def pack_actor_weights(policy: nn.Module, out: torch.Tensor | None = None) -> torch.Tensor | None:
+    """The float32 weight block of sit_policy_actor (include/sit.h) from a GaussianPolicy whose trunk
+    is the reference's default MLP (obs 10 -> 256 -> ReLU -> 256 -> ReLU -> 2; mlp.py:95-148,
+    main_ast.py:67), or None for any other architecture (those take the generic path)."""
+    net = getattr(policy, "net", None)
+    if net is None or getattr(policy, "act_dim", 1) != 1 or len(net) != 5:
+        return None
+    l1, r1, l2, r2, l3 = net
+    H = _lib.SIT_ACTOR_HIDDEN
+    shapes_ok = (isinstance(l1, nn.Linear) and isinstance(l2, nn.Linear) and isinstance(l3, nn.Linear)
+                 and isinstance(r1, nn.ReLU) and isinstance(r2, nn.ReLU)
+                 and tuple(l1.weight.shape) == (H, _lib.SIT_OBS_DIM) and tuple(l2.weight.shape) == (H, H)
+                 and tuple(l3.weight.shape) == (2, H) and l1.bias is not None and l2.bias is not None
+                 and l3.bias is not None)
+    if not shapes_ok:
+        return None
+    with torch.no_grad():
+        parts = [l1.weight.reshape(-1), l1.bias, l2.weight.t().reshape(-1), l2.bias, l3.weight.reshape(-1), l3.bias]
+        flat = torch.cat([t.detach().to(torch.float32).reshape(-1) for t in parts])
+        if out is None:
+            return flat.contiguous()
+        out.copy_(flat)
+        return out
+
+
 class PolicySampler:
     """Fused K-step launches in policy mode with the actor evaluated between launches.
 
     request_capacity bounds the envs served per launch (default n_env: every waiting env);
     envs beyond it keep waiting and re-request on the next launch.  The actor runs on a fixed
     number of rows (no host synchronisation); rows past the device-side request count are
-    scattered into a dummy slot."""
+    scattered into a dummy slot.
+
+    With the reference's default actor architecture (``pack_actor_weights``) the whole actor runs as
+    one HIP kernel (sit_policy_actor), which also clears the request count for the next launch;
+    ``fused_actor=False`` or any other architecture evaluates the network with PyTorch-ROCm.  The
+    fused path reads a packed copy of the weights: after an optimizer step call
+    ``refresh_weights()`` (``act()`` does it by itself outside HIP-graph replays)."""
 
     def __init__(self, env: VecMultiShipRLEnv, policy: nn.Module, chunk: int = 32, seed: int = 25450,
                  env_id_offset: int = 0, request_capacity: int | None = None, mask_horizon: int = 600,
-                 transition_capacity: int = 0, deterministic: bool = False, actor_dtype=None):
+                 transition_capacity: int = 0, deterministic: bool = False, actor_dtype=None,
+                 fused_actor: bool = True):
         self.env, self.policy, self.chunk, self.seed = env, policy, int(chunk), int(seed)
         self.env_id_offset, self.mask_horizon = int(env_id_offset), int(mask_horizon)
         self.transition_capacity, self.deterministic = int(transition_capacity), deterministic
@@ -107,6 +139,24 @@ class PolicySampler:
         self._one = torch.ones(cap, dtype=torch.int32, device=dev)
         self.out: dict = {}
         self.served = torch.zeros(1, dtype=torch.int64, device=dev)   # policy evaluations used
+        self._w = pack_actor_weights(policy) if fused_actor and self.actor_dtype == torch.float32 else None
+        if self._w is not None:
+            self._w = self._w.to(dev)
+            self._w_version = self._weights_version()
+            self._blocks_done = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    @property
+    def fused(self) -> bool:
+        return self._w is not None
+
+    def _weights_version(self):
+        return tuple((p.data_ptr(), p._version) for p in self.policy.parameters())
+
+    def refresh_weights(self):
+        """Re-pack the actor weights (after the policy's parameters changed)."""
+        if self._w is not None:
+            pack_actor_weights(self.policy, out=self._w)
+            self._w_version = self._weights_version()
 
     @property
     def env_steps(self) -> torch.Tensor:
@@ -116,7 +166,8 @@ class PolicySampler:
     def launch(self, want=("next_state", "reward", "done", "status", "action")):
         """One fused launch of `chunk` steps followed by the actor on the queued requests.
         Returns the launch's [K, n_env, ...] outputs (rows of waiting envs: status ST_NO_STEP)."""
-        self.io["request_count"].zero_()
+        if self._w is None:       # the fused actor clears the count itself
+            self.io["request_count"].zero_()
         self.env.rollout(self.chunk, seed=self.seed, env_id_offset=self.env_id_offset, out=self.out,
                          want=want, transition_capacity=self.transition_capacity,
                          mask_horizon=self.mask_horizon, policy_io=self.io)
@@ -141,11 +192,22 @@ class PolicySampler:
 
     @torch.no_grad()
     def act(self):
-        """Actor network (PyTorch-ROCm GEMMs) on the queued observations, then the squashed
-        Gaussian head and the scatter into the per-env action slots in one HIP kernel
-        (sit_policy_apply).  Policies without a `.net` (mu, log_sigma) trunk use the generic
-        path: forward() and a device-side scatter."""
+        """The actor on the queued observations and the scatter into the per-env action slots:
+        one HIP kernel (sit_policy_actor) for the default architecture; otherwise the network in
+        PyTorch-ROCm, then the squashed Gaussian head and the scatter in one HIP kernel
+        (sit_policy_apply), or for policies without a `.net` (mu, log_sigma) trunk forward() and a
+        device-side scatter."""
         io, env = self.io, self.env
+        if self._w is not None:
+            if not torch.cuda.is_current_stream_capturing() and self._weights_version() != self._w_version:
+                self.refresh_weights()
+            with torch.cuda.device(env.device):
+                env._call("sit_policy_actor", int(self._rows.numel()), self._w.data_ptr(), io["request_obs"].data_ptr(),
+                          io["request_noise"].data_ptr(), io["request_env"].data_ptr(),
+                          io["request_count"].data_ptr(), int(bool(self.deterministic)),
+                          io["policy_action"].data_ptr(), io["policy_ready"].data_ptr(), self.served.data_ptr(),
+                          self._blocks_done.data_ptr(), env._stream())
+            return
         obs = io["request_obs"] if self.actor_dtype == env.dtype else io["request_obs"].to(self.actor_dtype)
         net = getattr(self.policy, "net", None)
         if net is not None and getattr(self.policy, "act_dim", 1) == 1:

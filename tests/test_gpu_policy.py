@@ -6,6 +6,8 @@ reference's per-step loop (test_beds/main_ast.py:310-412, agent.select_action mo
 same policy and the same Philox noise.  Per env, the k-th executed GPU step must equal the
 oracle's k-th step: float64 within 1e-9 (per-field floors), discrete outputs identical.
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -171,3 +173,77 @@ def test_f32_policy_mode_sanity():
         assert torch.isfinite(out["reward"][live]).all()
     assert stepped == int(sm.env_steps.item())
     assert stepped > 0.8 * 20 * 32 * n_env
+
+
+def make_policy256(device):
+    torch.manual_seed(5)
+    pol = GaussianPolicy(hidden=(256, 256))
+    with torch.no_grad():
+        pol.net[0].weight.mul_(1e-3)
+    return pol.to(dtype=torch.float32, device=device)
+
+
+@pytest.mark.parametrize("precision,deterministic", [(32, False), (32, True), (64, False)])
+def test_fused_actor_matches_torch_float64(precision, deterministic):
+    """sit_policy_actor (the whole 10-256-256-2 actor + squashed head + scatter in one kernel)
+    against the same policy evaluated in float64 PyTorch on the queued rows: |action| error
+    <= 1e-5 (float32 actor); the request count is cleared and `served` advanced by the kernel."""
+    n_env = 2048
+    env = VecMultiShipRLEnv(scenario=make_scenario(n_env, cap=48, seed=7), precision=precision, device=DEV)
+    env.reset()
+    env.init_step()
+    pol = make_policy256(DEV)
+    ref_pol = copy.deepcopy(pol).double()
+    sm = PolicySampler(env, pol, chunk=32, seed=SEED, request_capacity=1024, deterministic=deterministic)
+    assert sm.fused
+    io = sm.io
+    checked = 0
+    for it in range(6):
+        env.rollout(sm.chunk, seed=sm.seed, env_id_offset=0, out=sm.out, policy_io=io)
+        torch.cuda.synchronize()
+        count = min(int(io["request_count"].item()), io["request_env"].numel())
+        obs = io["request_obs"][:count].double().clone()
+        noise = io["request_noise"][:count].double().clone()
+        envs = io["request_env"][:count].long().clone()
+        served0 = int(sm.served.item())
+        io["policy_ready"].zero_()
+        sm.act()
+        torch.cuda.synchronize()
+        assert int(io["request_count"].item()) == 0
+        assert int(sm.served.item()) == served0 + count
+        with torch.no_grad():
+            ref = ref_pol(obs, noise, deterministic=deterministic)[0][:, 0]
+        got = io["policy_action"][envs].double()
+        assert torch.all(io["policy_ready"][envs] == 1)
+        if count:
+            err = (got - ref).abs().max().item()
+            assert err <= 1e-5, f"launch {it}: fused actor max |err| {err:.3e} over {count} rows"
+            assert ref.abs().max().item() > (1e-3 if deterministic else 0.05)   # not all ~0
+        checked += count
+    assert checked >= n_env
+
+
+def test_fused_actor_policy_mode_sanity():
+    """C5 configuration on a small population: fused actor, graph capture, overlapped groups."""
+    n_env = 4096
+    samplers = []
+    for g in range(2):
+        env = VecMultiShipRLEnv(scenario=make_scenario(n_env, cap=48, seed=9, env_offset=g * n_env), precision=32,
+                                device=DEV)
+        env.reset()
+        env.init_step()
+        samplers.append(PolicySampler(env, make_policy256(DEV), chunk=32, seed=SEED, env_id_offset=g * n_env,
+                                      request_capacity=n_env // 4))
+    assert all(s.fused for s in samplers)
+    ov = OverlappedPolicySampler(samplers).capture(4)
+    before = [int(s.env_steps.item()) for s in samplers]
+    for _ in range(5):
+        outs = ov.replay()
+    torch.cuda.synchronize()
+    for s, b, out in zip(samplers, before, outs):
+        stepped = int(s.env_steps.item()) - b
+        assert stepped > 0.8 * 5 * 4 * 32 * n_env
+        st = out["status"].to(torch.int64) & 0xFFFFFFFF
+        live = (st & _lib.ST_NO_STEP) == 0
+        assert torch.isfinite(out["next_state"][live]).all()
+        assert int(s.served.item()) > n_env
