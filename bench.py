@@ -451,7 +451,7 @@ def bench_policy(args, rank, world, dev):
     torch.cuda.synchronize(dev)
     launch_ms = [a.elapsed_time(b) for row in ev for a, b in row]
     # the timed loop: HIP-graph replays of `per_graph` launches of every group
-    per_graph = max(1, min(args.graph_launches, args.steps // chunk))
+    per_graph = max(2, min(args.graph_launches, args.steps // chunk) // 2 * 2)   # even: 2-slot request counter
     runner.capture(per_graph)
     n_rep = max(1, args.steps // (chunk * per_graph))
     n_warm = max(1, args.warmup // (chunk * per_graph))

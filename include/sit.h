@@ -364,14 +364,15 @@ int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t 
  *            W2 transposed [256 in][256 out], b2 [256], W3 [2][256], b3 [2]
  *   obs      real[capacity][SIT_OBS_DIM] (the request_obs rows of sit_rollout_args)
  *   served   int64[1] or NULL: += min(*request_count, capacity)
- *   blocks_done int32[1] or NULL (zero-initialised scratch): when given, *request_count is reset to 0
- *            once every block has read it, ready for the next sit_rollout launch. */
+ *   clear_count int32[1] or NULL: set to 0 (one store, no grid-wide synchronisation).  With a
+ *            two-slot request counter the caller alternates slots between launches: sit_rollout i
+ *            appends to slot i%2, this call reads slot i%2 and clears slot (i+1)%2 for launch i+1. */
 #define SIT_ACTOR_HIDDEN 256
 #define SIT_ACTOR_WEIGHTS (SIT_ACTOR_HIDDEN * SIT_OBS_DIM + SIT_ACTOR_HIDDEN + SIT_ACTOR_HIDDEN * SIT_ACTOR_HIDDEN + \
                            SIT_ACTOR_HIDDEN + 2 * SIT_ACTOR_HIDDEN + 2)
 int sit_policy_actor(sit_handle* h, int32_t capacity, const float* weights, const void* obs, const void* noise,
-                     const int32_t* request_env, int32_t* request_count, int32_t deterministic,
-                     void* policy_action, int32_t* policy_ready, int64_t* served, int32_t* blocks_done,
+                     const int32_t* request_env, const int32_t* request_count, int32_t deterministic,
+                     void* policy_action, int32_t* policy_ready, int64_t* served, int32_t* clear_count,
                      void* stream);
 
 /* ---- state export / import (device blob) ------------------------------------------ */

@@ -7,12 +7,14 @@
 // separate library GEMMs plus elementwise kernels that was ~8 launches per act, ~40 % of C5's GPU
 // time; here it is one launch whose blocks past the device-side request count exit at once.
 //
-// Layout: one block of 256 threads (4 waves) per kActorRows request rows; thread j owns hidden
-// unit j of both layers.  Layer 1 reads the rows' observations from LDS; layer 2 streams W2^T
-// (row k = the 256 weights of input k, so one k is one coalesced 1 KiB read, L2-resident across
-// blocks) against the rows' layer-1 activations (LDS broadcast reads), two rows per packed FMA;
-// layer 3 is a block reduction (lane shuffles, then LDS across the waves).  FP32 throughout (the
-// reference actor's dtype); summation order differs from a GEMM library's, within 1e-5.
+// Layout: one block of 256 threads (4 waves) per kActorRows request rows.  Layer 1: thread j = hidden
+// unit j.  Layer 2 (99 % of the flops) is split over K: wave q takes inputs [64 q, 64 q + 64) for
+// all 256 units, lane l units 4l..4l+3, so each k is one coalesced 1 KiB float4 read of W2^T
+// (L2-resident across blocks, 16 rows in flight per lane) and one wave-uniform LDS broadcast of
+// the rows' activations feeds 16 packed FMAs; the four quarter sums meet in LDS in a fixed order.
+// Layer 3: 16 lanes per (row, output), then a 16-lane shuffle reduction.  FP32 throughout (the
+// reference actor's dtype); deterministic; summation order differs from a GEMM library's, well
+// within 1e-5.
 #pragma once
 
 #include "sit_device.h"
@@ -38,103 +40,135 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <typename T>
 __global__ __launch_bounds__(256) void k_policy_actor(int cap, const float* __restrict__ w, const T* __restrict__ obs,
                                                       const T* __restrict__ noise, const int32_t* __restrict__ req_env,
-                                                      int32_t* req_count, int deterministic, T* policy_action,
-                                                      int32_t* policy_ready, int n_env, unsigned long long* served,
-                                                      int32_t* blocks_done) {
-  __shared__ float s_obs[kActorRows][kActorObs];
-  __shared__ __align__(16) float s_h1[kActorRows][kActorHidden];
-  __shared__ float s_red[4][2 * kActorRows];
+                                                      const int32_t* __restrict__ req_count, int deterministic,
+                                                      T* policy_action, int32_t* policy_ready, int n_env,
+                                                      unsigned long long* served, int32_t* clear_count) {
+  constexpr int H = kActorHidden, R = kActorRows;
+  __shared__ float s_obs[R][kActorObs];
+  __shared__ __align__(16) f32x2 s_h1[R / 2][H];     // layer-1 activations, row pairs interleaved
+  __shared__ __align__(16) float s_h[R][H];          // layer-2 activations
+  __shared__ __align__(16) float s_part[4][R][H];    // layer-2 partial sums of the 4 K quarters
   const int j = threadIdx.x;
-  const int count = min(*req_count, cap);
-  const int row0 = blockIdx.x * kActorRows;
-  if (blockIdx.x == 0 && j == 0 && served) atomicAdd(served, (unsigned long long)max(count, 0));
+  const int row0 = blockIdx.x * R;
+  if (row0 >= cap) return;
+  // every independent global read is issued up front (one memory round trip instead of a chain):
+  // the request count, this block's observation rows (read whether or not they are valid), the
+  // layer-1 weights and the first W2^T batch
+  const int raw_count = *req_count;
+  const int orow = j / kActorObs, oi = j % kActorObs;
+  const bool oload = j < R * kActorObs && row0 + orow < cap;
+  const float ov = oload ? (float)obs[(size_t)(row0 + orow) * kActorObs + oi] : 0.0f;
+  float wr[kActorObs];
+#pragma unroll
+  for (int i = 0; i < kActorObs; ++i) wr[i] = w[kActorW1 + j * kActorObs + i];
+  const float b1 = w[kActorB1 + j];
+  const int q = j >> 6, l = j & 63;
+  const float4* w2 = reinterpret_cast<const float4*>(w + kActorW2T) + l;
+  const int kq = q * 64;
+  constexpr int KB = 32;                 // W2^T rows in flight per lane (two batches)
+  float4 wa[KB], wb[KB];
+#pragma unroll
+  for (int i = 0; i < KB; ++i) wa[i] = w2[(kq + i) * (H / 4)];
+  const int count = min(raw_count, cap);
+  if (blockIdx.x == 0 && j == 0) {
+    if (served) atomicAdd(served, (unsigned long long)max(count, 0));
+    // the other slot of the two-slot request counter: consumed by the previous actor launch,
+    // appended to by the next env launch (no block of this launch reads it)
+    if (clear_count) *clear_count = 0;
+  }
   if (row0 < count) {
-    const int nrow = min(kActorRows, count - row0);
-    if (j < kActorRows * kActorObs) {
-      const int r = j / kActorObs, i = j % kActorObs;
-      s_obs[r][i] = r < nrow ? (float)obs[(size_t)(row0 + r) * kActorObs + i] : 0.0f;
-    }
+    const int nrow = min(R, count - row0);
+    if (j < R * kActorObs) s_obs[orow][oi] = orow < nrow ? ov : 0.0f;
     __syncthreads();
-    // layer 1: h1 = relu(W1 obs + b1)
+    // layer 1 (thread j = hidden unit j): h1 = relu(W1 obs + b1)
     {
-      float wr[kActorObs];
+      const float b = b1;
 #pragma unroll
-      for (int i = 0; i < kActorObs; ++i) wr[i] = w[kActorW1 + j * kActorObs + i];
-      const float b = w[kActorB1 + j];
-#pragma unroll
-      for (int r = 0; r < kActorRows; ++r) {
+      for (int r = 0; r < R; ++r) {
         float acc = 0.0f;
 #pragma unroll
         for (int i = 0; i < kActorObs; ++i) acc = fmaf(wr[i], s_obs[r][i], acc);
-        s_h1[r][j] = fmaxf(acc + b, 0.0f);
+        s_h1[r >> 1][j][r & 1] = fmaxf(acc + b, 0.0f);
       }
     }
     __syncthreads();
-    // layer 2: h2 = relu(W2 h1 + b2), rows in pairs (packed FMA)
-    f32x2 acc[kActorRows / 2];
+    // layer 2, split-K: wave q sums inputs k in [64 q, 64 q + 64) for all 256 units, lane l owning
+    // units 4l..4l+3 (one coalesced float4 of W2^T per k); the layer-1 activations are wave-uniform
+    // LDS broadcast reads, each feeding 16 packed FMAs (row pairs)
+    {
+      f32x2 acc[4][R / 2];
 #pragma unroll
-    for (int p = 0; p < kActorRows / 2; ++p) acc[p] = f32x2{0.0f, 0.0f};
-    const float* w2t = w + kActorW2T + j;
-#pragma unroll 2
-    for (int k = 0; k < kActorHidden; k += 4) {
-      const float w0 = w2t[(k + 0) * kActorHidden], w1 = w2t[(k + 1) * kActorHidden];
-      const float w2 = w2t[(k + 2) * kActorHidden], w3 = w2t[(k + 3) * kActorHidden];
+      for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int p = 0; p < kActorRows / 2; ++p) {
-        const float4 ha = *reinterpret_cast<const float4*>(&s_h1[2 * p][k]);
-        const float4 hb = *reinterpret_cast<const float4*>(&s_h1[2 * p + 1][k]);
-        acc[p] = __builtin_elementwise_fma(f32x2{ha.x, hb.x}, f32x2{w0, w0}, acc[p]);
-        acc[p] = __builtin_elementwise_fma(f32x2{ha.y, hb.y}, f32x2{w1, w1}, acc[p]);
-        acc[p] = __builtin_elementwise_fma(f32x2{ha.z, hb.z}, f32x2{w2, w2}, acc[p]);
-        acc[p] = __builtin_elementwise_fma(f32x2{ha.w, hb.w}, f32x2{w3, w3}, acc[p]);
+        for (int p = 0; p < R / 2; ++p) acc[n][p] = f32x2{0.0f, 0.0f};
+#pragma unroll
+      for (int c = 0; c < 64 / KB; ++c) {
+        if (c + 1 < 64 / KB) {
+#pragma unroll
+          for (int i = 0; i < KB; ++i) wb[i] = w2[(kq + (c + 1) * KB + i) * (H / 4)];
+        }
+#pragma unroll
+        for (int g = 0; g < KB / 4; ++g) {
+          const int k = kq + c * KB + g * 4;
+          // (h[2p][k], h[2p+1][k]) pairs for k..k+3: two b128 broadcast reads per row pair
+          f32x2 hp[R / 2][4];
+#pragma unroll
+          for (int p = 0; p < R / 2; ++p) {
+            const float4 lo = *reinterpret_cast<const float4*>(&s_h1[p][k]);
+            const float4 hi = *reinterpret_cast<const float4*>(&s_h1[p][k + 2]);
+            hp[p][0] = f32x2{lo.x, lo.y}; hp[p][1] = f32x2{lo.z, lo.w};
+            hp[p][2] = f32x2{hi.x, hi.y}; hp[p][3] = f32x2{hi.z, hi.w};
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 wk = wa[g * 4 + i];
+            const float wn[4] = {wk.x, wk.y, wk.z, wk.w};
+#pragma unroll
+            for (int p = 0; p < R / 2; ++p)
+#pragma unroll
+              for (int n = 0; n < 4; ++n) acc[n][p] = __builtin_elementwise_fma(hp[p][i], f32x2{wn[n], wn[n]}, acc[n][p]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < KB; ++i) wa[i] = wb[i];
+      }
+#pragma unroll
+      for (int p = 0; p < R / 2; ++p) {
+        *reinterpret_cast<float4*>(&s_part[q][2 * p][4 * l]) = float4{acc[0][p].x, acc[1][p].x, acc[2][p].x, acc[3][p].x};
+        *reinterpret_cast<float4*>(&s_part[q][2 * p + 1][4 * l]) = float4{acc[0][p].y, acc[1][p].y, acc[2][p].y, acc[3][p].y};
       }
     }
-    const float b2 = w[kActorB2 + j];
-    const float v0 = w[kActorW3 + j], v1 = w[kActorW3 + kActorHidden + j];
-    // layer 3 partials: out[r][o] = b3[o] + sum_j W3[o][j] h2[r][j]
-    float part[2 * kActorRows];
+    __syncthreads();
+    {
+      const float b2 = w[kActorB2 + j];
 #pragma unroll
-    for (int p = 0; p < kActorRows / 2; ++p) {
-      const float h0 = fmaxf(acc[p].x + b2, 0.0f), h1 = fmaxf(acc[p].y + b2, 0.0f);
-      part[4 * p + 0] = h0 * v0;
-      part[4 * p + 1] = h0 * v1;
-      part[4 * p + 2] = h1 * v0;
-      part[4 * p + 3] = h1 * v1;
+      for (int r = 0; r < R; ++r)
+        s_h[r][j] = fmaxf(((s_part[0][r][j] + s_part[1][r][j]) + (s_part[2][r][j] + s_part[3][r][j])) + b2, 0.0f);
     }
+    __syncthreads();
+    // layer 3: 16 (row, output) pairs x 16 lanes, each lane 16 units, then a 16-lane reduction
+    {
+      const int pr = j >> 4, c = j & 15;
+      const int r = pr >> 1, o = pr & 1;
+      const float* v = w + kActorW3 + o * H + c * 16;
+      float sum = 0.0f;
 #pragma unroll
-    for (int q = 0; q < 2 * kActorRows; ++q) {
+      for (int i = 0; i < 16; ++i) sum = fmaf(s_h[r][c * 16 + i], v[i], sum);
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) part[q] += __shfl_xor(part[q], off, 64);
-    }
-    if ((j & 63) == 0) {
-#pragma unroll
-      for (int q = 0; q < 2 * kActorRows; ++q) s_red[j >> 6][q] = part[q];
+      for (int off = 8; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 16);
+      if (c == 0) s_part[0][0][pr] = sum + w[kActorB3 + o];
     }
     __syncthreads();
     if (j < nrow) {
-      const int r = j;
-      const float mu = w[kActorB3 + 0] + ((s_red[0][2 * r] + s_red[1][2 * r]) + (s_red[2][2 * r] + s_red[3][2 * r]));
-      const float ls_raw = w[kActorB3 + 1] + ((s_red[0][2 * r + 1] + s_red[1][2 * r + 1]) +
-                                              (s_red[2][2 * r + 1] + s_red[3][2 * r + 1]));
+      const float mu = s_part[0][0][2 * j], ls_raw = s_part[0][0][2 * j + 1];
       // normal.py:88-101 (log_sigma clipped to [-20, 2], reparameterised sample), tanh squash
       const float ls = fminf(fmaxf(ls_raw, -20.0f), 2.0f);
-      const int q = row0 + r;
-      const float x = deterministic ? mu : fmaf(expf(ls), (float)noise[q], mu);
-      const int e = req_env[q];
+      const int qrow = row0 + j;
+      const float x = deterministic ? mu : fmaf(expf(ls), (float)noise[qrow], mu);
+      const int e = req_env[qrow];
       if (e >= 0 && e < n_env) {
         policy_action[e] = (T)tanhf(x);
         policy_ready[e] = 1;
-      }
-    }
-  }
-  // the last block to finish clears the request count for the next env launch
-  if (blocks_done) {
-    __syncthreads();
-    if (j == 0) {
-      __threadfence();
-      if (atomicAdd(blocks_done, 1) == (int)gridDim.x - 1) {
-        atomicExch(req_count, 0);
-        atomicExch(blocks_done, 0);
       }
     }
   }
@@ -142,12 +176,12 @@ __global__ __launch_bounds__(256) void k_policy_actor(int cap, const float* __re
 
 template <typename T>
 int launch_policy_actor(sit_handle* h, int cap, const float* w, const void* obs, const void* noise,
-                        const int32_t* req_env, int32_t* req_count, int det, void* act, int32_t* ready,
-                        int64_t* served, int32_t* blocks_done, hipStream_t stream) {
+                        const int32_t* req_env, const int32_t* req_count, int det, void* act, int32_t* ready,
+                        int64_t* served, int32_t* clear_count, hipStream_t stream) {
   const int blocks = (cap + kActorRows - 1) / kActorRows;
   hipLaunchKernelGGL(k_policy_actor<T>, dim3(blocks), dim3(kActorHidden), 0, stream, cap, w, (const T*)obs,
                      (const T*)noise, req_env, req_count, det, (T*)act, ready, h->n_env,
-                     reinterpret_cast<unsigned long long*>(served), blocks_done);
+                     reinterpret_cast<unsigned long long*>(served), clear_count);
   return SIT_OK;
 }
 

@@ -101,8 +101,8 @@ int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t 
 }
 
 int sit_policy_actor(sit_handle* h, int32_t capacity, const float* weights, const void* obs, const void* noise,
-                     const int32_t* request_env, int32_t* request_count, int32_t deterministic,
-                     void* policy_action, int32_t* policy_ready, int64_t* served, int32_t* blocks_done,
+                     const int32_t* request_env, const int32_t* request_count, int32_t deterministic,
+                     void* policy_action, int32_t* policy_ready, int64_t* served, int32_t* clear_count,
                      void* stream) {
   if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
   if (capacity <= 0 || !weights || !obs || !request_env || !request_count || !policy_action || !policy_ready ||
@@ -110,10 +110,10 @@ int sit_policy_actor(sit_handle* h, int32_t capacity, const float* weights, cons
     return fail(h, SIT_E_INVALID, "policy_actor: bad arguments");
   int rc = h->precision == SIT_F64
                ? launch_policy_actor<double>(h, capacity, weights, obs, noise, request_env, request_count,
-                                             deterministic, policy_action, policy_ready, served, blocks_done,
+                                             deterministic, policy_action, policy_ready, served, clear_count,
                                              (hipStream_t)stream)
                : launch_policy_actor<float>(h, capacity, weights, obs, noise, request_env, request_count,
-                                            deterministic, policy_action, policy_ready, served, blocks_done,
+                                            deterministic, policy_action, policy_ready, served, clear_count,
                                             (hipStream_t)stream);
   if (rc) return rc;
   HIP_TRY(h, hipGetLastError());

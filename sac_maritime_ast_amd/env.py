@@ -191,7 +191,7 @@ class VecMultiShipRLEnv:
             t = out.get(k)
             if t is None or tuple(t.shape) != shp or t.dtype != dt:
                 out[k] = torch.empty(shp, dtype=dt, device=self.device)
-        if "done_count" in out:
+        if "done_count" in want:
             out["done_count"].zero_()
         ra = _lib.RolloutArgs()
         ra.n_steps, ra.auto_reset, ra.seed, ra.env_id_offset = K, int(bool(auto_reset)), int(seed), int(env_id_offset)

@@ -132,9 +132,13 @@ class PolicySampler:
             "request_env": torch.zeros(cap, dtype=torch.int32, device=dev),
             "request_noise": torch.zeros(cap, dtype=dt, device=dev),
             "request_obs": torch.zeros((cap, _lib.SIT_OBS_DIM), dtype=dt, device=dev),
-            "request_count": torch.zeros(1, dtype=torch.int32, device=dev),
             "env_steps": torch.zeros(1, dtype=torch.int64, device=dev),
         }
+        # two-slot request counter: launch i appends to slot i % 2 (io["request_count"] is a view
+        # of the current slot); the fused actor of launch i clears the other slot for launch i + 1
+        self._counts = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._slot = 0
+        self.io["request_count"] = self._counts[0:1]
         self._rows = torch.arange(cap, device=dev, dtype=torch.int32)
         self._one = torch.ones(cap, dtype=torch.int32, device=dev)
         self.out: dict = {}
@@ -143,7 +147,6 @@ class PolicySampler:
         if self._w is not None:
             self._w = self._w.to(dev)
             self._w_version = self._weights_version()
-            self._blocks_done = torch.zeros(1, dtype=torch.int32, device=dev)
 
     @property
     def fused(self) -> bool:
@@ -166,19 +169,26 @@ class PolicySampler:
     def launch(self, want=("next_state", "reward", "done", "status", "action")):
         """One fused launch of `chunk` steps followed by the actor on the queued requests.
         Returns the launch's [K, n_env, ...] outputs (rows of waiting envs: status ST_NO_STEP)."""
-        if self._w is None:       # the fused actor clears the count itself
+        p = self._slot
+        self.io["request_count"] = self._counts[p:p + 1]
+        if self._w is None:       # the fused actor clears the slot of the next launch itself
             self.io["request_count"].zero_()
         self.env.rollout(self.chunk, seed=self.seed, env_id_offset=self.env_id_offset, out=self.out,
                          want=want, transition_capacity=self.transition_capacity,
                          mask_horizon=self.mask_horizon, policy_io=self.io)
         self.act()
+        self._slot ^= 1
         return self.out
 
-    def capture(self, n_launch: int = 1, want=("next_state", "reward", "done", "status", "action")):
+    def capture(self, n_launch: int = 2, want=("next_state", "reward", "done", "status", "action")):
         """Record `n_launch` launches (env kernel + actor) into one HIP graph; replay() then runs
         them with a single submission (the per-launch host work of ctypes and ~10 torch ops
-        otherwise bounds short chunks).  The output buffers are those of the last launch."""
+        otherwise bounds short chunks).  The output buffers are those of the last launch.
+        n_launch must be even (the request-counter slots alternate per launch)."""
+        if n_launch % 2:
+            raise ValueError("capture an even number of launches (two-slot request counter)")
         self.launch(want)                     # allocate every buffer outside the capture
+        self.launch(want)
         torch.cuda.synchronize(self.env.device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
@@ -206,7 +216,7 @@ class PolicySampler:
                           io["request_noise"].data_ptr(), io["request_env"].data_ptr(),
                           io["request_count"].data_ptr(), int(bool(self.deterministic)),
                           io["policy_action"].data_ptr(), io["policy_ready"].data_ptr(), self.served.data_ptr(),
-                          self._blocks_done.data_ptr(), env._stream())
+                          self._counts[1 - self._slot:2 - self._slot].data_ptr(), env._stream())
             return
         obs = io["request_obs"] if self.actor_dtype == env.dtype else io["request_obs"].to(self.actor_dtype)
         net = getattr(self.policy, "net", None)
@@ -253,9 +263,12 @@ class OverlappedPolicySampler:
     def env_steps(self) -> torch.Tensor:
         return sum(sm.env_steps for sm in self.samplers)
 
-    def capture(self, n_launch: int = 1, want=("next_state", "reward", "done", "status", "action")):
+    def capture(self, n_launch: int = 2, want=("next_state", "reward", "done", "status", "action")):
         """One HIP graph holding `n_launch` rounds of every group (forked onto the groups'
-        streams inside the capture, joined at the end)."""
+        streams inside the capture, joined at the end); n_launch even (PolicySampler.capture)."""
+        if n_launch % 2:
+            raise ValueError("capture an even number of launches (two-slot request counter)")
+        self.launch(want)
         self.launch(want)
         torch.cuda.synchronize(self.streams[0].device)
         self.graph = torch.cuda.CUDAGraph()
