@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -1079,6 +1080,27 @@ int fail(sit_handle* h, int code, const char* fmt, ...) {
     hipError_t e_ = (call);                                                                 \
     if (e_ != hipSuccess) return fail((h), SIT_E_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
   } while (0)
+
+// Device memory of the setup calls (sit_create / sit_load_* / sit_destroy).  Sanitizer builds
+// (-DSIT_HOST_MEMORY_TEST, tools/sanitize.sh: host ASan/UBSan) back it with host memory, so that
+// the host logic -- argument checks, blob layout, the map index, route and scenario staging --
+// runs and is checked on a machine without a GPU; kernels are not launched in that build.
+#ifdef SIT_HOST_MEMORY_TEST
+hipError_t setup_device(int* d) { *d = 0; return hipSuccess; }
+hipError_t setup_alloc(unsigned char** p, size_t n) {
+  *p = static_cast<unsigned char*>(std::malloc(n ? n : 1));
+  return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t setup_free(void* p) { std::free(p); return hipSuccess; }
+hipError_t setup_zero(void* p, size_t n) { std::memset(p, 0, n); return hipSuccess; }
+hipError_t setup_upload(void* dst, const void* src, size_t n) { std::memcpy(dst, src, n); return hipSuccess; }
+#else
+hipError_t setup_device(int* d) { return hipGetDevice(d); }
+hipError_t setup_alloc(unsigned char** p, size_t n) { return hipMalloc(p, n); }
+hipError_t setup_free(void* p) { return hipFree(p); }
+hipError_t setup_zero(void* p, size_t n) { return hipMemset(p, 0, n); }
+hipError_t setup_upload(void* dst, const void* src, size_t n) { return hipMemcpy(dst, src, n, hipMemcpyHostToDevice); }
+#endif
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 size_t real_size(const sit_handle* h) { return h->precision == SIT_F64 ? 8 : 4; }

@@ -221,7 +221,7 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
   h->n_env = n_env;
   h->cap = wpt_capacity;
   h->p = *p;
-  hipError_t e = hipGetDevice(&h->device);
+  hipError_t e = setup_device(&h->device);
   if (e != hipSuccess) { fail(nullptr, SIT_E_HIP, "hipGetDevice: %s", hipGetErrorString(e)); delete h; return SIT_E_HIP; }
   const size_t rs = real_size(h);
   size_t off = 0;
@@ -246,12 +246,12 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
   h->scen_ab_alpha = so; so = align256(so + (size_t)n_env * 8);
   h->scen_initial = so; so = align256(so + (size_t)n_env * SIT_OBS_DIM * rs);
   h->scen_bytes = so;
-  if (hipMalloc(&h->blob, h->blob_bytes) != hipSuccess || hipMalloc(&h->scen, h->scen_bytes) != hipSuccess) {
+  if (setup_alloc(&h->blob, h->blob_bytes) != hipSuccess || setup_alloc(&h->scen, h->scen_bytes) != hipSuccess) {
     fail(nullptr, SIT_E_NOMEM, "hipMalloc of %zu + %zu bytes failed", h->blob_bytes, h->scen_bytes);
     sit_destroy(h);
     return SIT_E_NOMEM;
   }
-  if (hipMemset(h->blob, 0, h->blob_bytes) != hipSuccess || hipMemset(h->scen, 0, h->scen_bytes) != hipSuccess) {
+  if (setup_zero(h->blob, h->blob_bytes) != hipSuccess || setup_zero(h->scen, h->scen_bytes) != hipSuccess) {
     fail(nullptr, SIT_E_HIP, "hipMemset failed");
     sit_destroy(h);
     return SIT_E_HIP;
@@ -262,9 +262,9 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
 
 void sit_destroy(sit_handle* h) {
   if (!h) return;
-  if (h->blob) (void)hipFree(h->blob);
-  if (h->scen) (void)hipFree(h->scen);
-  if (h->map) (void)hipFree(h->map);
+  if (h->blob) (void)setup_free(h->blob);
+  if (h->scen) (void)setup_free(h->scen);
+  if (h->map) (void)setup_free(h->map);
   delete h;
 }
 
@@ -524,9 +524,9 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
     if (rs == 8) reinterpret_cast<double*>(host.data() + h->map_bbox)[i] = bbox[i];
     else reinterpret_cast<float*>(host.data() + h->map_bbox)[i] = (float)bbox[i];
   }
-  if (h->map) { (void)hipFree(h->map); h->map = nullptr; }
-  HIP_TRY(h, hipMalloc(&h->map, o));
-  HIP_TRY(h, hipMemcpy(h->map, host.data(), o, hipMemcpyHostToDevice));
+  if (h->map) { (void)setup_free(h->map); h->map = nullptr; }
+  HIP_TRY(h, setup_alloc(&h->map, o));
+  HIP_TRY(h, setup_upload(h->map, host.data(), o));
   h->n_poly = n_poly;
   h->n_vert = nv;
   h->have_map = true;
@@ -570,13 +570,13 @@ int sit_load_routes(sit_handle* h, const double* wpt_ne, const int32_t* n_wpt) {
   const size_t tcnt = (size_t)2 * cap * n;
   auto tn = conv(tab.data(), tcnt), te = conv(tab.data() + tcnt, tcnt);
   auto en = conv(end.data(), (size_t)2 * n), ee = conv(end.data() + (size_t)2 * n, (size_t)2 * n);
-  HIP_TRY(h, hipMemcpy(h->blob + h->off[F_WN], tn.data(), tn.size(), hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemcpy(h->blob + h->off[F_WE], te.data(), te.size(), hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemcpy(h->scen + h->scen_end_n, en.data(), en.size(), hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemcpy(h->scen + h->scen_end_e, ee.data(), ee.size(), hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemcpy(h->scen + h->scen_nw0, nw0.data(), nw0.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemcpy(h->scen + h->scen_ab_len, ab_len.data(), (size_t)n * 8, hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemcpy(h->scen + h->scen_ab_alpha, ab_alpha.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+  HIP_TRY(h, setup_upload(h->blob + h->off[F_WN], tn.data(), tn.size()));
+  HIP_TRY(h, setup_upload(h->blob + h->off[F_WE], te.data(), te.size()));
+  HIP_TRY(h, setup_upload(h->scen + h->scen_end_n, en.data(), en.size()));
+  HIP_TRY(h, setup_upload(h->scen + h->scen_end_e, ee.data(), ee.size()));
+  HIP_TRY(h, setup_upload(h->scen + h->scen_nw0, nw0.data(), nw0.size() * 4));
+  HIP_TRY(h, setup_upload(h->scen + h->scen_ab_len, ab_len.data(), (size_t)n * 8));
+  HIP_TRY(h, setup_upload(h->scen + h->scen_ab_alpha, ab_alpha.data(), (size_t)n * 8));
   h->have_routes = true;
   return SIT_OK;
 }
@@ -608,8 +608,8 @@ int sit_load_initial(sit_handle* h, const double* init) {
     return out;
   };
   auto a = conv(sc), b = conv(ist);
-  HIP_TRY(h, hipMemcpy(h->scen + h->scen_init, a.data(), a.size(), hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemcpy(h->scen + h->scen_initial, b.data(), b.size(), hipMemcpyHostToDevice));
+  HIP_TRY(h, setup_upload(h->scen + h->scen_init, a.data(), a.size()));
+  HIP_TRY(h, setup_upload(h->scen + h->scen_initial, b.data(), b.size()));
   h->have_init = true;
   return SIT_OK;
 }

@@ -121,3 +121,62 @@ def test_scenario_matches_survey():
     assert np.abs(d).max() <= 100.0 and np.abs(big.init[:, :, 2] - sc.init[:, :, 2]).max() <= 0.05
     o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
     assert o.ab_len[0] == pytest.approx(914.3973146174434, rel=1e-14)
+
+
+def _host_handle(lib, n_env=64, cap=32, precision=32):
+    """A handle for the setup calls, or None where sit_create needs a GPU that is absent (the
+    sanitizer build, tools/sanitize.sh, backs the setup memory with host memory instead)."""
+    h = ctypes.c_void_p()
+    p = config.params()
+    rc = lib.sit_create(ctypes.byref(p), n_env, cap, precision, ctypes.byref(h))
+    if rc != 0:
+        return None
+    return h
+
+
+@pytest.mark.parametrize("precision", [32, 64])
+def test_setup_calls_host_logic(precision):
+    """sit_load_map / sit_load_routes / sit_load_initial / sit_map_info / sit_state_field on the
+    scenario of SURVEY §8(d): argument checks, the spatial index build and the blob layout (no
+    kernel is launched).  Runs where a handle can be created: the GPU box, and the host-memory
+    sanitizer build (tools/sanitize.sh, ASan + UBSan)."""
+    lib = _lib.load()
+    n_env, cap = 64, 32
+    h = _host_handle(lib, n_env, cap, precision)
+    if h is None:
+        pytest.skip("sit_create needs a HIP device (use the sanitizer build for host-only runs)")
+    try:
+        sc = scenario.make_scenario(n_env, cap=cap)
+        polys = [np.ascontiguousarray(p, dtype=np.float64) for p in sc.polys]
+        offs = np.zeros(len(polys) + 1, dtype=np.int32)
+        offs[1:] = np.cumsum([len(p) for p in polys])
+        verts = np.ascontiguousarray(np.concatenate(polys))
+        vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        assert lib.sit_load_map(h, len(polys), vp(offs), vp(verts)) == 0, lib.sit_last_error(h)
+        bad = offs.copy()
+        bad[1] = 2
+        assert lib.sit_load_map(h, len(polys), vp(bad), vp(verts)) == _lib.SIT_E_INVALID
+        info = np.zeros(6, dtype=np.int64)
+        assert lib.sit_map_info(h, vp(info), 6) == 0
+        assert info[0] > 0 and info[1] > 1000 and info[2] > 1000 and info[5] >= info[0]
+        routes = np.ascontiguousarray(sc.routes, dtype=np.float64)
+        n_wpt = np.ascontiguousarray(sc.n_wpt, dtype=np.int32)
+        assert lib.sit_load_routes(h, vp(routes), vp(n_wpt)) == 0, lib.sit_last_error(h)
+        bad_n = n_wpt.copy()
+        bad_n[3, 1] = cap + 1
+        assert lib.sit_load_routes(h, vp(routes), vp(bad_n)) == _lib.SIT_E_INVALID
+        init = np.ascontiguousarray(sc.init, dtype=np.float64)
+        assert lib.sit_load_initial(h, vp(init)) == 0, lib.sit_last_error(h)
+        nbytes = ctypes.c_size_t()
+        assert lib.sit_state_bytes(h, ctypes.byref(nbytes)) == 0
+        end = 0
+        for f in range(lib.sit_state_nfields()):
+            name, off, dt, cnt = ctypes.c_char_p(), ctypes.c_size_t(), ctypes.c_int32(), ctypes.c_int64()
+            assert lib.sit_state_field(h, f, ctypes.byref(name), ctypes.byref(off), ctypes.byref(dt),
+                                       ctypes.byref(cnt)) == 0
+            assert off.value % 256 == 0 and off.value >= end and cnt.value > 0
+            el = (precision // 8) if dt.value == _lib.SIT_DT_REAL else 4
+            end = off.value + cnt.value * el
+        assert end <= nbytes.value
+    finally:
+        lib.sit_destroy(h)
