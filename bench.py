@@ -156,12 +156,40 @@ def cpu_baseline(seconds, seed, workers):
         res.append(json.loads(outp.strip().splitlines()[-1]))
     total = sum(r["env_steps"] for r in res)
     dt = max(r["seconds"] for r in res)
+    # BASELINE.md CPU plan 2(a): the reference-equivalent scalar loop (one env, one process, one
+    # core), and through the calibration ratio measured in the build container
+    # (oracle/calibrate.py: reference / restatement at one env on one core) the reference's own
+    # estimated speed on this host, where the reference cannot run
+    sp = subprocess.run([sys.executable, "-c", CPU_WORKER, ROOT, "1", str(max(2.0, seconds / 2)), str(seed), "0"],
+                        capture_output=True, env=env, text=True)
+    scalar = None
+    if sp.returncode == 0:
+        r1 = json.loads(sp.stdout.strip().splitlines()[-1])
+        scalar = {"value": r1["env_steps"] / r1["seconds"], "unit": "env-steps/s", "cores": 1,
+                  "sample": f"oracle/sit_oracle.py with one env, {r1['steps']} steps, {r1['seconds']:.1f} s"}
+        cal = latest_calibration()
+        if cal:
+            ratio = cal["env_steps_per_s"]["ratio_reference_over_restatement"]
+            scalar["reference_estimate"] = scalar["value"] * ratio
+            scalar["calibration"] = {"ratio_reference_over_restatement": ratio, "source": cal["_file"],
+                                     "measured_on": cal["cpu_model"]}
     return {"value": total / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "per_core_value": float(np.mean([r["env_steps"] / r["seconds"] for r in res])),
             "cpu_model": _cpu_model(),
             "sample": f"oracle/sit_oracle.py float64 NumPy, {cores} single-threaded processes x {n_env} envs x "
                       f"~{int(np.mean([r['steps'] for r in res]))} steps each (synthetic sampler, auto-reset), "
-                      f"{dt:.1f} s wall"}
+                      f"{dt:.1f} s wall",
+            "scalar_1core": scalar}
+
+
+def latest_calibration():
+    """The newest profiles/*cpu_calibration.json (oracle/calibrate.py), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*cpu_calibration.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    d["_file"] = os.path.relpath(files[-1], ROOT)
+    return d
 
 
 def stats_of(launch_ms):

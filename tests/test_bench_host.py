@@ -1,4 +1,6 @@
 """Host-side pieces of bench.py (no GPU): the algorithmic-bytes model and the CPU-baseline leg."""
+import pytest
+
 import bench
 
 
@@ -18,6 +20,10 @@ def test_cpu_baseline_workers_report():
     assert r["kind"] == "port" and r["unit"] == "env-steps/s"
     assert r["cores"] == 2 and r["value"] > 0 and r["per_core_value"] > 0
     assert "2 single-threaded processes" in r["sample"]
+    sc = r["scalar_1core"]
+    assert sc["cores"] == 1 and sc["value"] > 0
+    if bench.latest_calibration() is not None:
+        assert sc["reference_estimate"] == pytest.approx(sc["value"] * sc["calibration"]["ratio_reference_over_restatement"])
 
 
 def _run_bench(*argv, env_extra=None, timeout=300):
