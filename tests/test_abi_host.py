@@ -180,3 +180,19 @@ def test_setup_calls_host_logic(precision):
         assert end <= nbytes.value
     finally:
         lib.sit_destroy(h)
+
+
+def test_jittered_starts_fixture_n4096():
+    """The benchmark scenario's jittered starts for N = 4096, committed by
+    tests/golden/make_scenario_fixture.py: reproduced bit for bit, also by shards of the
+    population (env_offset), within +-100 m and +-0.05 rad of the unjittered starts."""
+    d = np.load(os.path.join(ROOT, "tests", "golden", "scenario_jitter_4096.npz"))
+    sc = scenario.make_scenario(4096, seed=int(d["seed"]))
+    assert np.array_equal(sc.init[:, :, 0], d["start_north"])
+    assert np.array_equal(sc.init[:, :, 1], d["start_east"])
+    assert np.array_equal(sc.init[:, :, 2], d["start_yaw"])
+    half = scenario.make_scenario(2048, seed=int(d["seed"]), env_offset=2048)
+    assert np.array_equal(half.init[:, :, :3], sc.init[2048:, :, :3])
+    base = scenario.make_scenario(1, jitter=False).init[0]
+    assert np.abs(d["start_north"] - base[:, 0]).max() <= 100.0
+    assert np.abs(d["start_yaw"] - base[:, 2]).max() <= 0.05
