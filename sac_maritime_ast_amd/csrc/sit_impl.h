@@ -382,6 +382,9 @@ __device__ __forceinline__ void iw_point(double n, double e, double ab_len, doub
 }
 
 constexpr int kExplicit = 0, kSynth = 1, kPolicy = 2;
+// wave-uniform switches of the step loop (bits 0-4: the output arrays present)
+constexpr uint32_t kUfTrans = 1u << 5, kUfDoneCnt = 1u << 6, kUfAutoReset = 1u << 7, kUfMaskH = 1u << 8,
+                   kUfCollBias = 1u << 9, kUfBlackout = 1u << 10;
 constexpr uint32_t kSampGeBit = 1u << 28;   // exchange-only: obstacle sampling distance >= AB_len
 
 // One wave's K steps: TYPE 0 steps the ships under test, TYPE 1 the obstacle ships.  The ship type
@@ -480,6 +483,13 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   const int outs = __builtin_amdgcn_readfirstlane((a.io.next_state ? 1 : 0) | (a.io.reward ? 2 : 0) |
                                                   (a.io.done ? 4 : 0) | (a.io.status ? 8 : 0) |
                                                   (a.io.action_out ? 16 : 0));
+  // the loop's wave-uniform switches in one SGPR, made opaque at every iteration (below): the
+  // compiler then tests a bit where a switch is used instead of hoisting each one out of the loop
+  // as a 64-bit lane mask, which spilled ~40 SGPRs into VGPR lanes (v_readlane in the loop)
+  uint32_t uf = (uint32_t)outs | (a.io.transitions ? kUfTrans : 0u) | (a.io.done_count ? kUfDoneCnt : 0u) |
+                (a.io.auto_reset ? kUfAutoReset : 0u) | (a.io.mask_horizon > 0 ? kUfMaskH : 0u) |
+                (c.collision_bias ? kUfCollBias : 0u) | (c.sg_mode != SIT_SG_MOTOR ? kUfBlackout : 0u);
+  uf = __builtin_amdgcn_readfirstlane(uf);
   T* p_ns = (outs & 1) ? a.io.next_state + (size_t)env * SIT_OBS_DIM + (type == 0 ? 0 : 6) : nullptr;
   T* p_rw = (outs & 2) ? a.io.reward + env : nullptr;
   uint8_t* p_dn = (outs & 4) ? a.io.done + env : nullptr;
@@ -498,6 +508,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
 #endif
 
   for (int step = 0; step < a.io.n_steps; ++step) {
+    asm volatile("" : "+s"(uf));
     const size_t row = (size_t)step * n_env + env;
     Xchg<T>& x = xs[step & 1];
     // ---------------- own ship ----------------
@@ -602,7 +613,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         T rudder, thr, psi_ref;
         const T i1_0 = s.i1, i2_0 = s.i2;   // pre-step integrals (blackout knife edge)
         guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
-        if (c.collision_bias) {          // is_collision_imminent() on all-zero states (Q1)
+        if (uf & kUfCollBias) {          // is_collision_imminent() on all-zero states (Q1)
           thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
           rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
         }
@@ -612,7 +623,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         // float64 where the float32 margin is inside the float32 band (always for the float64 handle)
         mech = rpm_fails<T, MACH>(c, cs.x, s.w, o_rpm);
         // MOTOR (PTI): load_me = min(total, ME capacity) <= ME capacity, so no blackout ever (Q7)
-        if (c.sg_mode != SIT_SG_MOTOR) {
+        if (uf & kUfBlackout) {
           blk = o_pme > c.blackout_kw;
           if (!kIsF32<T> || xabs(o_pme - c.blackout_kw) <= T(1e-4) * (xabs(o_pme) + T(1)))
             blk = power_me_kw_exact(c.sg_mode, cs.x, throttle_exact(cs.x, s.u, v_des, i1_0, i2_0,
@@ -709,7 +720,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
       s.stop = stop;
       if (type == 1) {
         int slot = -1;
-        if (a.io.transitions && sac) slot = atomicAdd(a.io.transition_count, 1);
+        if ((uf & kUfTrans) && sac) slot = atomicAdd(a.io.transition_count, 1);
         x.slot[lane] = slot;
       }
       x.n[type][lane] = s.n;
@@ -727,8 +738,8 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
     // ---------------- env level: shared reward, outputs ----------------
     bool env_done = false;
     if (MODE == kPolicy && act && !live && type == 0) {   // no step taken this row
-      if (outs & 8) *p_st = SIT_ST_NO_STEP;
-      if (outs & 4) *p_dn = 0;
+      if (uf & 8) *p_st = SIT_ST_NO_STEP;
+      if (uf & 4) *p_dn = 0;
       if (stall_now) {
         const int q = x.slot[lane];
         if (q < a.io.request_capacity)
@@ -748,8 +759,8 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         const T reward = r_nt + r_term + x.r_nto[lane] + x.r_o[lane] + r_snt + rs;
         const uint32_t status = ((bt | bo) & ~(kStopBit | kDoneBit | kSampGeBit)) | (coll ? SIT_ST_COLLISION : 0u);
 #ifndef SIT_ABLATE_STORES
-        if (outs & 2) *p_rw = reward;
-        if (outs & 4) *p_dn = env_done ? 1 : 0;
+        if (uf & 2) *p_rw = reward;
+        if (uf & 4) *p_dn = env_done ? 1 : 0;
 #endif
         const int slot = x.slot[lane];
         if (slot >= 0 && slot < a.io.transition_capacity) {
@@ -757,21 +768,21 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
           for (int j = 0; j < 6; ++j) rec[j] = lo[j];
           rec[11] = reward;
           rec[12] = s.n; rec[13] = s.e; rec[14] = s.psi; rec[15] = o_rpm; rec[16] = o_ect; rec[17] = o_pme;
-          const bool horizon_hit = a.io.mask_horizon > 0 && ep_step + 2 == a.io.mask_horizon;
+          const bool horizon_hit = (uf & kUfMaskH) && ep_step + 2 == a.io.mask_horizon;
           rec[22] = (horizon_hit || !env_done) ? T(1) : T(0);
         }
 #ifndef SIT_ABLATE_STORES
-        if (outs & 8) *p_st = status;
+        if (uf & 8) *p_st = status;
 #endif
 #ifndef SIT_ABLATE_STORES
-        if (outs & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_rpm); store2(p_ns + 4, o_ect, o_pme); }
+        if (uf & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_rpm); store2(p_ns + 4, o_ect, o_pme); }
 #endif
       } else {
 #ifndef SIT_ABLATE_STORES
-        if (outs & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_ect); }
+        if (uf & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_ect); }
 #endif
 #ifndef SIT_ABLATE_STORES
-        if (outs & 16) { store2(p_ao, iwn, iwe); store2(p_ao + 2, angle_or_nan(has_ang, (T)ang), sac ? T(1) : T(0)); }
+        if (uf & 16) { store2(p_ao, iwn, iwe); store2(p_ao + 2, angle_or_nan(has_ang, (T)ang), sac ? T(1) : T(0)); }
 #endif
         const int slot = x.slot[lane];
         if (slot >= 0 && slot < a.io.transition_capacity) {
@@ -792,11 +803,11 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         // the next step is a sampling event at an episode start or once the sampling distance
         // reaches AB_len while the obstacle ship runs (the obstacle lane's own test, exchanged)
         const bool obs_stop = (bo & kStopBit) || coll;
-        need = ((bo & kSampGeBit) && !obs_stop) || (a.io.auto_reset && env_done);
+        need = ((bo & kSampGeBit) && !obs_stop) || ((uf & kUfAutoReset) && env_done);
       }
     }
     // episode-done count: one ballot + popcount per wave, one atomic per wave
-    if (type == 0 && a.io.done_count) {
+    if (type == 0 && (uf & kUfDoneCnt)) {
       const unsigned long long m = __ballot(env_done);
       if (lane == 0 && m) atomicAdd(a.io.done_count + step, (int)__popcll(m));
     }
@@ -808,7 +819,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
 #ifdef SIT_ABLATE_RESET
       if (false) {
 #else
-      if (a.io.auto_reset && env_done) {
+      if ((uf & kUfAutoReset) && env_done) {
 #endif
         // reset() (MSRL_Env.py:147-188) from the register copies
         s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Quick GPU check: selected test files (one process, per-test limits), then one default bench run.
-#   usage: tools/gpu_quick.sh "<pytest args>" [bench args]
+#   usage: [K=<pytest -k expr>] tools/gpu_quick.sh "<test paths>" [bench args]
 set -u
 mkdir -p gpurun_out
 T=${1:-tests}
 shift
-timeout -k 10 600 python -u -m pytest $T -m gpu -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 600 python -u -m pytest $T ${K:+-k "$K"} -m gpu -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
   > gpurun_out/quick_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
