@@ -10,9 +10,11 @@ git show "$rev:include/sit.h" > "$d/include/sit.h"
 git show "$rev:sac_maritime_ast_amd/csrc/sit_device.h" > "$d/csrc/sit_device.h"
 git show "$rev:sac_maritime_ast_amd/csrc/sit_kernels.hip" > "$d/csrc/sit_kernels.hip"
 # single-TU build (no -DSIT_SPLIT_F32): pass "-Xarch_device -ffast-math" to match the float32 TU
-if git cat-file -e "$rev:sac_maritime_ast_amd/csrc/sit_impl.h" 2>/dev/null; then
-  git show "$rev:sac_maritime_ast_amd/csrc/sit_impl.h" > "$d/csrc/sit_impl.h"
-fi
+for f in sit_impl.h sit_actor.h; do
+  if git cat-file -e "$rev:sac_maritime_ast_amd/csrc/$f" 2>/dev/null; then
+    git show "$rev:sac_maritime_ast_amd/csrc/$f" > "$d/csrc/$f"
+  fi
+done
 (cd /tmp && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared \
    -fno-hip-fp32-correctly-rounded-divide-sqrt -I "$d/include" -I "$d/csrc" "$@" \
    "$d/csrc/sit_kernels.hip" -o "$OLDPWD/build_diag/libsit_$name.so")
