@@ -519,6 +519,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
     int dv[7] = {0, 0, 0, 0, 0, 0, 0};
 #endif
     bool sac = false, init_f = false;
+    int tslot = -1;                    // transition record slot of this step (obstacle lane)
     double ang = 0.0;                  // the sampled angle; has_ang: drawn on device this step
     double act_n = 0.0;                // the SAC action of the event: ang / (pi / 6), in [-1, 1]
     bool has_ang = false;
@@ -573,6 +574,19 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
           sac = a.io.sac_update[row] != 0;
           iwn = a.io.action_ne[2 * row];
           iwe = a.io.action_ne[2 * row + 1];
+        }
+        // replay-transition slot of a sampling event, allocated here at the start of the step (one
+        // atomic per wave, ranks by lane): its latency overlaps guidance, dynamics and predicates
+        // instead of stalling the exchange before the barrier
+        if (uf & kUfTrans) {
+          const unsigned long long m = __ballot(sac);
+          if (m) {
+            const int lead = __builtin_ctzll(m);
+            int base = 0;
+            if (lane == lead) base = atomicAdd(a.io.transition_count, (int)__popcll(m));
+            base = __shfl(base, lead);
+            if (sac) tslot = base + (int)__popcll(m & ((1ull << lane) - 1ull));
+          }
         }
         // obs_step (MSRL_Env.py:287-402)
         if (s.stop) {
@@ -718,11 +732,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         if (done) bits |= SIT_ST_OBS_DONE;
       }
       s.stop = stop;
-      if (type == 1) {
-        int slot = -1;
-        if ((uf & kUfTrans) && sac) slot = atomicAdd(a.io.transition_count, 1);
-        x.slot[lane] = slot;
-      }
+      if (type == 1) x.slot[lane] = tslot;
       x.n[type][lane] = s.n;
       x.e[type][lane] = s.e;
       x.bits[type][lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u) |
