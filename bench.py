@@ -501,7 +501,8 @@ def bench_policy(args, rank, world, dev):
     kern_ms = float(np.median(launch_ms))
     rs = 4 if args.precision == 32 else 8
     alg = algorithmic_bytes_per_launch(per, chunk, rs, 3.0, 5.0, "rollout")
-    rl = roofline(alg, kern_ms, None)
+    pmc = latest_pmc(args.precision, "policy", per, chunk)
+    rl = roofline(alg, kern_ms, pmc)
     rl["launch_ms"] = stats_of(launch_ms)
     rl["note"] = "per group launch (n_env / groups envs), groups run concurrently on separate streams"
     rl["kernel_ms_statistic"] = "median over 16 eager launches (HIP events on each group's stream)"
