@@ -8,11 +8,11 @@ tools/gpu_steps.sh \
  prof_c3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --- \
  prof_c5 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode policy --- \
  prof_step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_step -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step --- \
- pmc 900 bash tools/pmc.sh --warmup 40000 --steps 5000
+ pmc 900 bash tools/pmc.sh
 rc=$?
-python3 tools/pmc_summary.py gpurun_out/pmc k_env_steps > gpurun_out/pmc_summary.json
+python3 tools/pmc_summary.py gpurun_out/pmc k_env_steps 8 > gpurun_out/pmc_summary.json
 python3 tools/make_profile_json.py gpurun_out/pmc_summary.json gpurun_out/${R}_pmc_f32_rollout.json \
-  --steps-per-launch 5000 --round ${R#r} --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh (5 passes) on bench.py --warmup 40000 --steps 5000 (chunk 5000; 9 launches averaged per pass)"
+  --steps-per-launch 20000 --round ${R#r} --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh (5 passes) on the default bench.py (chunk 20000; the 3 timed launches averaged per pass, the 8 warm-up launches skipped)"
 rm -f gpurun_out/prof_*/run_kernel_trace.csv
 find gpurun_out/pmc -name "*.csv" -size +1M -delete
 du -sh gpurun_out
