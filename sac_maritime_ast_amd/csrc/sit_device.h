@@ -408,8 +408,13 @@ struct Ship {
 // 180-189; LOS_guidance.py:88-121).  Returns rudder, throttle and |e_ct|.
 // LOS_guidance.py:110-120 in the reference's float64 arithmetic from the (float32) state: the
 // cross-track error |e|, the (clamped) e / Delta and whether the integrator accepts it
+// inlined: as an out-of-line call it cost 2 % of C3 (call frame and register saves around a
+// branch that is almost never taken)
+#ifndef SIT_LOS_EXACT_INLINE
+#define SIT_LOS_EXACT_INLINE __attribute__((always_inline))
+#endif
 template <typename T>
-__device__ __attribute__((noinline)) void los_exact(const ConstsX64& x, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
+__device__ SIT_LOS_EXACT_INLINE void los_exact(const ConstsX64& x, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
                                                     double& ect_abs, double& q, double& sum, bool& accept) {
   // sin / cos of the leg angle as dy / L, dx / L in IEEE float64: equal to the reference's
   // math.sin / math.cos of math.atan2 (:110-113) within an ulp or two, so e_ct is within ~1e-12 m of
@@ -873,8 +878,11 @@ __device__ __forceinline__ int fine_class(const Consts<T>& c, const Map<T>& m, T
 // GEOS's count over a cell's live edges in float64 at the exact point (nd, ed), starting from the
 // cell's constant parity.  Out of line: one copy serves every call site (it runs only where the
 // float32 count is unsure, or on the float64 handle), keeping the step loop's code footprint small.
+#ifndef SIT_PIP_EXACT_INLINE
+#define SIT_PIP_EXACT_INLINE __attribute__((noinline))
+#endif
 template <typename T>
-__device__ __attribute__((noinline)) bool pip_live_exact(const Edge<T>* edge, const uint8_t* live, int cnt,
+__device__ SIT_PIP_EXACT_INLINE bool pip_live_exact(const Edge<T>* edge, const uint8_t* live, int cnt,
                                                          uint32_t par, double nd, double ed) {
   uint32_t onb = 0;
   for (int k = 0; k < cnt; ++k) {
