@@ -12,7 +12,7 @@ tools/gpu_steps.sh \
 rc=$?
 python3 tools/pmc_summary.py gpurun_out/pmc k_env_steps 8 > gpurun_out/pmc_summary.json
 python3 tools/make_profile_json.py gpurun_out/pmc_summary.json gpurun_out/${R}_pmc_f32_rollout.json \
-  --steps-per-launch 20000 --round ${R#r} --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh (5 passes) on the default bench.py (chunk 20000; the 3 timed launches averaged per pass, the 8 warm-up launches skipped)"
+  --steps-per-launch 40000 --round ${R#r} --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh (5 passes) on the default bench.py (chunk 40000; the 3 timed launches averaged per pass, the 8 warm-up launches skipped)"
 rm -f gpurun_out/prof_*/run_kernel_trace.csv
 find gpurun_out/pmc -name "*.csv" -size +1M -delete
 du -sh gpurun_out
