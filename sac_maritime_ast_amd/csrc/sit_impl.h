@@ -381,6 +381,14 @@ __device__ __forceinline__ void iw_point(double n, double e, double ab_len, doub
   iwe = e + ab_len * sin(ab_alpha + ang);
 }
 
+// the sampler's seed made opaque where it is used: otherwise the compiler hoists Philox's ten-round
+// key schedule (18 uniform words) out of the step loop and spills it into VGPR lanes
+__device__ __forceinline__ uint64_t opaque_seed(uint64_t seed) {
+  uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
+  asm volatile("" : "+s"(lo), "+s"(hi));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 constexpr int kExplicit = 0, kSynth = 1, kPolicy = 2;
 // wave-uniform switches of the step loop (bits 0-4: the output arrays present)
 constexpr uint32_t kUfTrans = 1u << 5, kUfDoneCnt = 1u << 6, kUfAutoReset = 1u << 7, kUfMaskH = 1u << 8,
@@ -408,7 +416,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   // LDS: the map blob (edges, index, classes).  Route tables stay in HBM (Route caches the
   // active leg); keeping the block under 64 KB of LDS matters: a larger allocation measured
   // ~1.75x slower at the same occupancy-limited grid.
-  const Map<T> map = LDSMAP ? stage_map(a, smem) : a.map;
+  Map<T> map = LDSMAP ? stage_map(a, smem) : a.map;
   const int lane = threadIdx.x & (kWave - 1);
   constexpr int type = TYPE;
   const int n_env = a.n_env;
@@ -509,6 +517,8 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
 
   for (int step = 0; step < a.io.n_steps; ++step) {
     asm volatile("" : "+s"(uf));
+    // the map's switches likewise (compared where used, not held as lane masks)
+    asm volatile("" : "+s"(map.use_index), "+s"(map.use_cells), "+s"(map.n_edge), "+s"(map.n_poly));
     const size_t row = (size_t)step * n_env + env;
     Xchg<T>& x = xs[step & 1];
     // ---------------- own ship ----------------
@@ -536,7 +546,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         x.slot[lane] = q;
         if (q < a.io.request_capacity) {
           a.io.request_env[q] = env;
-          a.io.request_noise[q] = (T)sampler_normal(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
+          a.io.request_noise[q] = (T)sampler_normal(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
           for (int j = 0; j < 4; ++j) a.io.request_obs[(size_t)q * SIT_OBS_DIM + 6 + j] = lo[j];
         }
       }
@@ -562,7 +572,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
           init_f = (ep_step == 0);
           sac = init_f || ((double)samp >= ab_len && !s.stop);
           if (sac) {                     // mode-0 action U[-1, 1] (uniform_policy.py:20-22) scaled by pi/6
-            const double u01 = sampler_uniform(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
+            const double u01 = sampler_uniform(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
             act_n = u01 * 2.0 - 1.0;
             ang = act_n * (M_PI / 6.0);
             has_ang = true;
