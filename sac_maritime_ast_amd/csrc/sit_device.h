@@ -96,6 +96,14 @@ constexpr int kWave = 64;         // CDNA wavefront
 // envs per step-kernel block: one wave of test ships + one wave of obstacle ships, the first
 // kEnvsPerBlock lanes of each wave active
 constexpr int kEnvsPerBlock = SIT_ENVS_PER_BLOCK;
+#ifndef SIT_GROUPS
+#define SIT_GROUPS 1
+#endif
+// env groups (wave pairs) per step-kernel block; the groups of a block share one LDS map copy
+constexpr int kGroups = SIT_GROUPS;
+#ifndef SIT_MIN_WAVES
+#define SIT_MIN_WAVES 1   // step kernel: waves per SIMD the register budget must allow
+#endif
 constexpr int kMaxPolyVerts = 256;
 constexpr int kMaxPolys = 32;
 

@@ -420,7 +420,9 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   const int lane = threadIdx.x & (kWave - 1);
   constexpr int type = TYPE;
   const int n_env = a.n_env;
-  const int env = blockIdx.x * kEnvsPerBlock + lane;
+  const int group = kGroups > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 7) : 0;
+  const int env = (blockIdx.x * kGroups + group) * kEnvsPerBlock + lane;
+  xs += 2 * group;
   const bool act = lane < kEnvsPerBlock && env < n_env;
   const int sid = type * n_env + env;
 
@@ -667,6 +669,9 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
 #elif defined(SIT_ABLATE_HULL)        // diagnostic: distance kept, hull test removed
       const T dobst = distance_indexed(c, map, s.n, s.e);
       const bool terrain = false;
+#elif defined(SIT_ABLATE_DIST)        // diagnostic: distance removed, hull test by its four corners
+      const T dobst = T(1000);
+      const bool terrain = hull_corners(c, map, s.n, s.e);
 #else
       SIT_PH(0);
       int cell_c;
@@ -918,11 +923,11 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
 // MACH: the handle's machinery model as a kernel template argument (a runtime branch on it inside
 // the step loop measured ~4% slower: it splits the scheduling regions of guidance and dynamics)
 template <typename T, int MODE, bool LDSMAP, bool LOG, int MACH>
-__global__ __launch_bounds__(128) void k_env_steps(const KArgs<T> a) {
+__global__ __launch_bounds__(128 * kGroups, SIT_MIN_WAVES) void k_env_steps(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ Xchg<T> xs[2];
+  __shared__ Xchg<T> xs[2 * kGroups];
   __shared__ Consts<T> cs;
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) env_steps<T, MODE, LDSMAP, LOG, 0, MACH>(a, smem, xs, cs);
+  if ((__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 1) == 0) env_steps<T, MODE, LDSMAP, LOG, 0, MACH>(a, smem, xs, cs);
   else env_steps<T, MODE, LDSMAP, LOG, 1, MACH>(a, smem, xs, cs);
 }
 
@@ -1320,11 +1325,11 @@ template <typename T>
 int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   KArgs<T> a = make_args<T>(h);
   a.io = io;
-  const int blocks = (h->n_env + kEnvsPerBlock - 1) / kEnvsPerBlock;
+  const int blocks = (h->n_env + kEnvsPerBlock * kGroups - 1) / (kEnvsPerBlock * kGroups);
   const int mode = io.action_ne ? kExplicit : (io.policy_action ? kPolicy : kSynth);
   // the map (edges, index, classes) is staged in LDS when it fits the budget next to the
   // static exchange buffers; otherwise the predicates read it through the caches
-  const size_t stat = sizeof(Xchg<T>) * 2 + sizeof(Consts<T>) + 256;
+  const size_t stat = sizeof(Xchg<T>) * 2 * kGroups + sizeof(Consts<T>) + 256;
   const bool lds_map = map_lds_bytes(h) + stat <= kLdsBudget;
   const size_t lds = lds_map ? map_lds_bytes(h) : 0;
   auto go = [&](auto kern) -> int {
@@ -1335,7 +1340,7 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
       HIP_TRY(h, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       h->lds_attr[slot] = (int)lds;
     }
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(128), lds, stream, a);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(128 * kGroups), lds, stream, a);
     return SIT_OK;
   };
   auto pick_mach = [&](auto mode_tag, auto mach_tag) -> int {
