@@ -275,7 +275,7 @@ __device__ __forceinline__ double angle_or_nan(bool has, double a) {
 //           sampling event without a fresh action waits for the rest of the launch and queues
 //           a request; the next launch consumes the action the policy wrote for it)
 // ---------------------------------------------------------------------------------------
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SPLIT)
 // Diagnostic builds only (tools/diag_paths.py): [type][0..15] predicate path statistics,
 // [type][16..23] shader-clock cycles per step phase (wave lane 0).
 __device__ unsigned long long g_sit_diag[2][32];
@@ -931,6 +931,8 @@ __global__ __launch_bounds__(128 * kGroups, SIT_MIN_WAVES) void k_env_steps(cons
   else env_steps<T, MODE, LDSMAP, LOG, 1, MACH>(a, smem, xs, cs);
 }
 
+#include "sit_split.h"
+
 // MultiShipRLEnv.init_step for masked envs (one thread per ship)
 template <typename T>
 __global__ __launch_bounds__(256) void k_init_step(const KArgs<T> a, const uint8_t* mask) {
@@ -1090,6 +1092,7 @@ struct sit_handle {
   int lds_attr[24] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
                       -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
+  int lds_attr_split[2] = {-1, -1};   // dynamic-LDS size of k_env_steps_split per machinery model
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
   double fx0 = 0, fy0 = 0, finvx = 0, finvy = 0;
@@ -1319,6 +1322,7 @@ int ready(sit_handle* h) {
 // LDS budget of one step-kernel block: two blocks (4 waves, one per SIMD) must fit the CU's
 // 160 KB; above 80 KB only one block fits and the grid runs in two rounds (~1.75x slower)
 constexpr size_t kLdsBudget = 80 * 1024;
+constexpr size_t kLdsSplitMax = 160 * 1024;   // the CU's LDS: one block of the pipelined kernel per CU
 size_t map_lds_bytes(const sit_handle* h) { return (h->map_bytes + 255) & ~size_t(255); }
 
 template <typename T>
@@ -1352,6 +1356,28 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
     if (a.c.mach_simpl) return pick_mach(mode_tag, std::integral_constant<int, 1>{});
     return pick_mach(mode_tag, std::integral_constant<int, 0>{});
   };
+  // SIT_STEP_KERNEL=pipelined in the environment selects the two-waves-per-ship kernel
+  // (sit_split.h) for the synthetic sampler with auto-reset, without the trajectory log, when the
+  // map and its exchange ring fit one block's LDS.  Measured slower than k_env_steps at C3
+  // (1.47e10 vs 1.62e10 env-steps/s), so it is not the default.
+  const char* sel = getenv("SIT_STEP_KERNEL");
+  const bool pipelined = sel && strcmp(sel, "pipelined") == 0;
+  const size_t lds_split = split_lds_bytes<T>(h->map_bytes);
+  if (pipelined && mode == kSynth && !io.log && io.auto_reset && h->use_index &&
+      lds_split + sizeof(Consts<T>) + 256 <= kLdsSplitMax) {
+    const int mach = a.c.mach_simpl ? 1 : 0;
+    const void* kern = mach ? reinterpret_cast<const void*>(&k_env_steps_split<T, 1>)
+                            : reinterpret_cast<const void*>(&k_env_steps_split<T, 0>);
+    if (h->lds_attr_split[mach] != (int)lds_split) {
+      HIP_TRY(h, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_split));
+      h->lds_attr_split[mach] = (int)lds_split;
+    }
+    const int blocks2 = (h->n_env + 2 * kWave - 1) / (2 * kWave);
+    if (mach) hipLaunchKernelGGL((k_env_steps_split<T, 1>), dim3(blocks2), dim3(512), lds_split, stream, a);
+    else hipLaunchKernelGGL((k_env_steps_split<T, 0>), dim3(blocks2), dim3(512), lds_split, stream, a);
+    HIP_TRY(h, hipGetLastError());
+    return SIT_OK;
+  }
   int rc;
   if (mode == kSynth) rc = pick(std::integral_constant<int, kSynth>{});
   else if (mode == kPolicy) rc = pick(std::integral_constant<int, kPolicy>{});
