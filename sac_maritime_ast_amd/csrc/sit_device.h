@@ -639,12 +639,33 @@ __device__ __forceinline__ T power_me_kw(const Consts<T>& c, T thr) {
 
 // update_differentials + integrate_differentials; sp, cp = sin/cos of the pre-step heading
 // (computed by the caller at the start of the step, off the guidance dependency chain) (ship_model.py:624-643, ship_engine.py:355-395)
+// The post-step position needs only the pre-step state (forward Euler of eta_dot = R(psi) nu):
+// the step kernel computes it at the start of the step and issues the map lookups of that
+// position before guidance and dynamics (their LDS latency then overlaps the step's arithmetic);
+// ship_dynamics_pos stores exactly that position.
+template <typename T>
+__device__ __forceinline__ void euler_position(const Consts<T>& c, const Ship<T>& s, T sp, T cp, T& n1, T& e1) {
+  const T d_n = cp * s.u - sp * s.v;
+  const T d_e = sp * s.u + cp * s.v;
+  n1 = s.n + d_n * c.dt;
+  e1 = s.e + d_e * c.dt;
+}
+
+template <typename T, int MACH = -1>
+__device__ __forceinline__ void ship_dynamics_pos(const Consts<T>& c, Ship<T>& s, T thr, T rudder, T sp, T cp, T n1,
+                                                  T e1);
+
 template <typename T, int MACH = -1>
 __device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T thr, T rudder, T sp, T cp) {
+  T n1, e1;
+  euler_position(c, s, sp, cp, n1, e1);
+  ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
+}
+
+template <typename T, int MACH>
+__device__ __forceinline__ void ship_dynamics_pos(const Consts<T>& c, Ship<T>& s, T thr, T rudder, T sp, T cp, T n1,
+                                                  T e1) {
   const T u = s.u, v = s.v, r = s.r, w = s.w;
-  // kinematics: eta_dot = R(psi) nu
-  const T d_n = cp * u - sp * v;
-  const T d_e = sp * u + cp * v;
   T d_w, thrust;
   if (simpl_of<MACH>(c)) {
     // SimplifiedMachineryModel.update_thrust_force (ship_engine.py:423-428): w is the thrust force
@@ -681,9 +702,9 @@ __device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T 
   const T f0 = mv * r - yv * r - (c.d_u + c.ku * u) * ur + tau_u + thrust;
   const T f1 = -mu * r + xu * r - (c.d_v + c.kv * v) * vr + tau_v + f_rv;
   const T f2 = -(mv * u - mu * v) - (-yv * ur + xu * vr) - (c.d_r + c.kr * r) * r + tau_n + f_rr;
-  // Euler (utils.py:50-53)
-  s.n = s.n + d_n * c.dt;
-  s.e = s.e + d_e * c.dt;
+  // Euler (utils.py:50-53); the position from euler_position
+  s.n = n1;
+  s.e = e1;
   s.psi = s.psi + r * c.dt;
   s.u = u + (c.inv_m11 * f0) * c.dt;
   s.v = v + (c.inv_m22 * f1) * c.dt;
@@ -816,6 +837,58 @@ __device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
 #pragma unroll 1
   for (int g = 0; g < ng; ++g) {
     q = grp[g];
+    const T d0 = edge_dist2(m.edge[q.x & 0xffu], e, n);
+    const T d1 = edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n);
+    const T d2 = edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n);
+    const T d3 = edge_dist2(m.edge[q.x >> 24], e, n);
+    const T d4 = edge_dist2(m.edge[q.y & 0xffu], e, n);
+    best = xmin(best, xmin(xmin(xmin(d0, d1), xmin(d2, d3)), d4));
+  }
+  return xsqrt(best);
+}
+
+// distance_indexed in three stages, so the step kernel can issue the LDS lookups early and use
+// them late: the grid cell record and the class-grid word (pf_cell), the first candidate group's
+// edge records (pf_edges), the distances (pf_finish; same candidates, same min order, same value
+// as distance_indexed)
+template <typename T>
+__device__ __forceinline__ int fine_lookup(const Consts<T>& c, const Map<T>& m, T n, T e, int& cell, uint32_t& word);
+
+template <typename T>
+struct DistPf {
+  bool ok;             // inside the grid, index present
+  uint2 q;             // the cell record
+  Edge<T> g[5];        // the first group's edges
+  int cls, cell_f;     // class-grid lookup of the same point (fine_lookup)
+  uint32_t word_f;
+};
+template <typename T>
+__device__ __forceinline__ void pf_cell(const Consts<T>& c, const Map<T>& m, T n, T e, DistPf<T>& p) {
+  const T fx = (e - c.gx0) * c.ginvx, fy = (n - c.gy0) * c.ginvy;
+  p.ok = m.use_index && fx >= T(0) && fx < T(kGrid) && fy >= T(0) && fy < T(kGrid);
+  const int cell = p.ok ? (int)fy * kGrid + (int)fx : 0;
+  p.q = reinterpret_cast<const uint2*>(m.idx)[cell];
+  p.cls = fine_lookup(c, m, n, e, p.cell_f, p.word_f);
+}
+template <typename T>
+__device__ __forceinline__ void pf_edges(const Map<T>& m, DistPf<T>& p) {
+  p.g[0] = m.edge[p.q.x & 0xffu];
+  p.g[1] = m.edge[(p.q.x >> 8) & 0xffu];
+  p.g[2] = m.edge[(p.q.x >> 16) & 0xffu];
+  p.g[3] = m.edge[p.q.x >> 24];
+  p.g[4] = m.edge[p.q.y & 0xffu];
+}
+template <typename T>
+__device__ __forceinline__ T pf_finish(const Map<T>& m, const DistPf<T>& p, T n, T e) {
+  if (!p.ok) return distance_to_polys(m, n, e);
+  const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (p.q.y >> 16);
+  const int ng = (int)((p.q.y >> 8) & 0xffu);
+  T best = xmin(xmin(xmin(edge_dist2(p.g[0], e, n), edge_dist2(p.g[1], e, n)),
+                     xmin(edge_dist2(p.g[2], e, n), edge_dist2(p.g[3], e, n))),
+                edge_dist2(p.g[4], e, n));
+#pragma unroll 1
+  for (int g = 0; g < ng; ++g) {
+    const uint2 q = grp[g];
     const T d0 = edge_dist2(m.edge[q.x & 0xffu], e, n);
     const T d1 = edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n);
     const T d2 = edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n);

@@ -389,6 +389,9 @@ __device__ __forceinline__ uint64_t opaque_seed(uint64_t seed) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+#ifndef SIT_PF_EDGES_EARLY
+#define SIT_PF_EDGES_EARLY 0   // 1: the candidate edges loaded right after guidance (measured slower)
+#endif
 constexpr int kExplicit = 0, kSynth = 1, kPolicy = 2;
 // wave-uniform switches of the step loop (bits 0-4: the output arrays present)
 constexpr uint32_t kUfTrans = 1u << 5, kUfDoneCnt = 1u << 6, kUfAutoReset = 1u << 7, kUfMaskH = 1u << 8,
@@ -556,6 +559,14 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
     const bool live = act && !stalled;
     T sp = T(0), cp = T(1);
     if (live) xsincos(s.psi, &sp, &cp);    // heading trig of the step, off the guidance chain
+    // the post-step position (a function of the pre-step state) and its map lookups, issued now:
+    // their LDS latency overlaps guidance and dynamics (the predicates below use them)
+    T n1 = s.n, e1 = s.e;
+    DistPf<T> pf;
+    if (live) {
+      if (type == 0 || !s.stop) euler_position(c, s, sp, cp, n1, e1);
+      pf_cell(c, map, n1, e1, pf);
+    }
     if (live) {
       ++n_stepped;
       if (type == 1) {
@@ -609,6 +620,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
           s.ticks += 2;                  // stop path: next_time() twice, no integration (Q10)
           o_rpm = s.lrpm; o_ect = s.lect; o_pme = s.lpme;
           ect_over = (double)o_ect > cs.x.e_tol;
+          if (SIT_PF_EDGES_EARLY) pf_edges(map, pf);
         } else {
           if (sac) {                     // update_route: insert at index -1 (Q16)
             if (!rt.insert(iwn, iwe, s.k, a.cap)) bits |= SIT_ST_ROUTE_OVERFLOW;
@@ -617,6 +629,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
           const T pre_n = s.n, pre_e = s.e;
           T rudder, thr, psi_ref;
           guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+          if (SIT_PF_EDGES_EARLY) pf_edges(map, pf);
           o_rpm = s.w * c.rpm_k;
           o_pme = power_me_kw(c, thr);
           s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
@@ -624,7 +637,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
             store_log_row<T, MACH>(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
             for (int kk = 0; kk < SIT_LOG_KEYS; ++kk) a.st.last_log[kk * row_step + env] = p_lg[kk * row_step];
           }
-          ship_dynamics<T, MACH>(c, s, thr, rudder, sp, cp);
+          ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
           if (!init_f) {                 // distance between the last two stored positions
             const T dn = pre_n - ppn, de = pre_e - ppe;
             const T d = xsqrt(dn * dn + de * de);
@@ -639,6 +652,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         T rudder, thr, psi_ref;
         const T i1_0 = s.i1, i2_0 = s.i2;   // pre-step integrals (blackout knife edge)
         guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+        if (SIT_PF_EDGES_EARLY) pf_edges(map, pf);
         if (uf & kUfCollBias) {          // is_collision_imminent() on all-zero states (Q1)
           thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
           rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
@@ -658,7 +672,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         }
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
         if (p_lg) store_log_row<T, MACH>(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
-        ship_dynamics<T, MACH>(c, s, thr, rudder, sp, cp);
+        ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
         s.ticks += 1;
       }
 
@@ -674,12 +688,10 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
       const bool terrain = hull_corners(c, map, s.n, s.e);
 #else
       SIT_PH(0);
-      int cell_c;
-      uint32_t word_c;
-      const int cls_c = fine_lookup(c, map, s.n, s.e, cell_c, word_c);
-      const T dobst = distance_indexed(c, map, s.n, s.e);
+      if (!SIT_PF_EDGES_EARLY) pf_edges(map, pf);
+      const T dobst = pf_finish(map, pf, s.n, s.e);
       SIT_PH(1);
-      const bool terrain = hull_in_terrain_cls(c, map, s.n, s.e, dobst, cls_c, cell_c, word_c);
+      const bool terrain = hull_in_terrain_cls(c, map, s.n, s.e, dobst, pf.cls, pf.cell_f, pf.word_f);
       SIT_PH(2);
 #endif
 #ifdef SIT_DIAG_PATHS
