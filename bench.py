@@ -73,6 +73,8 @@ def parse():
                     help="single-threaded oracle processes (the GPU box's CPU share is 16 cores per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--transitions", action="store_true",
+                    help="N = 1: write the replay transitions too (every rank writes them at N > 1)")
     ap.add_argument("--launch-trace", action="store_true", help="print every launch's kernel ms to stderr")
     args = ap.parse_args()
     if args.chunk is None:
@@ -353,6 +355,7 @@ def bench_rollout(args, rank, world, dev):
     # Records beyond it are counted and reported ("dropped").
     tcap = max(n_env, n_env * chunk // 192)
     gather = AsyncTransitionGather(tcap, 24, env.dtype, dev, world) if (world > 1 and not args.no_gather) else None
+    local_tr = args.transitions and gather is None
     out = {}
     launch_no = [0]
 
@@ -382,7 +385,7 @@ def bench_rollout(args, rank, world, dev):
             if ev_pair:
                 ev_pair[0].record(stream)
             env.rollout(chunk, seed=args.seed, env_id_offset=offset, out=out,
-                        transition_capacity=tcap if gather else 0)
+                        transition_capacity=tcap if (gather or local_tr) else 0)
             if ev_pair:
                 ev_pair[1].record(stream)
             if gather:     # counts now, the valid records once this launch's counts are on the host
@@ -430,6 +433,9 @@ def bench_rollout(args, rank, world, dev):
         "roofline": rl,
         "roofline_valu": roofline_valu(kern_ms, pmc, n_env, chunk) if args.mode == "rollout" else None,
     }
+    if local_tr:
+        cnt = int(out["transition_count"].item())
+        res["config"]["transitions"] = {"records_last_launch": cnt, "capacity": tcap, "dropped_last_launch": max(0, cnt - tcap)}
     if gather is not None:
         stats = torch.tensor([gather.gathered - gathered0, gather.dropped() - dropped0], dtype=torch.float64,
                              device=dev)
