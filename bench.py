@@ -313,7 +313,7 @@ def roofline_valu(kern_ms, pmc, n_env, chunk):
     if per is None:
         return {"bound": "valu-issue", "achieved": None, "peak": VALU_PEAK_INST_S, "unit": "wave-instr/s",
                 "frac": None, "note": "no PMC summary for this configuration under profiles/"}
-    waves = 2 * ((n_env + 63) // 64)
+    waves = pmc.get("waves") or 2 * ((n_env + 63) // 64)   # the profiled kernel's waves (SQ_WAVES)
     inst = per * waves * chunk
     achieved = inst / (kern_ms * 1e-3)
     return {"bound": "valu-issue", "achieved": achieved, "peak": VALU_PEAK_INST_S, "unit": "wave-instr/s",

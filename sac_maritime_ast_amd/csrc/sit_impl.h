@@ -944,6 +944,7 @@ __global__ __launch_bounds__(128 * kGroups, SIT_MIN_WAVES) void k_env_steps(cons
 }
 
 #include "sit_split.h"
+#include "sit_sync.h"
 
 // MultiShipRLEnv.init_step for masked envs (one thread per ship)
 template <typename T>
@@ -1104,7 +1105,8 @@ struct sit_handle {
   int lds_attr[24] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
                       -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
-  int lds_attr_split[2] = {-1, -1};   // dynamic-LDS size of k_env_steps_split per machinery model
+  int lds_attr_split[2] = {-1, -1};
+  int lds_attr_sync[2] = {-1, -1};    // the same for k_env_steps_sync
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
   double fx0 = 0, fy0 = 0, finvx = 0, finvy = 0;
@@ -1368,12 +1370,30 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
     if (a.c.mach_simpl) return pick_mach(mode_tag, std::integral_constant<int, 1>{});
     return pick_mach(mode_tag, std::integral_constant<int, 0>{});
   };
-  // SIT_STEP_KERNEL=pipelined in the environment selects the two-waves-per-ship kernel
-  // (sit_split.h) for the synthetic sampler with auto-reset, without the trajectory log, when the
-  // map and its exchange ring fit one block's LDS.  Measured slower than k_env_steps at C3
-  // (1.47e10 vs 1.62e10 env-steps/s), so it is not the default.
+  // SIT_STEP_KERNEL=pipelined: the speculative two-waves-per-ship kernel (sit_split.h); measured
+  // slower than k_env_steps at C3 (1.47e10 vs 1.62e10 env-steps/s).
+  // Default for the synthetic sampler with auto-reset (the C3/C4 workload): k_env_steps_sync
+  // (sit_sync.h), two waves per ship with the map predicates on their own wave (+0.9 % on C3).
+  // SIT_STEP_KERNEL=classic selects k_env_steps, =pipelined the speculative kernel of sit_split.h.
   const char* sel = getenv("SIT_STEP_KERNEL");
   const bool pipelined = sel && strcmp(sel, "pipelined") == 0;
+  const bool synced = !(sel && (strcmp(sel, "classic") == 0 || pipelined));
+  const size_t lds_sync = sync_lds_bytes<T>(h->map_bytes);
+  if (synced && mode == kSynth && !io.log && io.auto_reset && h->use_index &&
+      lds_sync + sizeof(Consts<T>) + 256 <= kLdsSplitMax) {
+    const int mach = a.c.mach_simpl ? 1 : 0;
+    const void* kern = mach ? reinterpret_cast<const void*>(&k_env_steps_sync<T, 1>)
+                            : reinterpret_cast<const void*>(&k_env_steps_sync<T, 0>);
+    if (h->lds_attr_sync[mach] != (int)lds_sync) {
+      HIP_TRY(h, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sync));
+      h->lds_attr_sync[mach] = (int)lds_sync;
+    }
+    const int blocks2 = (h->n_env + 2 * kWave - 1) / (2 * kWave);
+    if (mach) hipLaunchKernelGGL((k_env_steps_sync<T, 1>), dim3(blocks2), dim3(512), lds_sync, stream, a);
+    else hipLaunchKernelGGL((k_env_steps_sync<T, 0>), dim3(blocks2), dim3(512), lds_sync, stream, a);
+    HIP_TRY(h, hipGetLastError());
+    return SIT_OK;
+  }
   const size_t lds_split = split_lds_bytes<T>(h->map_bytes);
   if (pipelined && mode == kSynth && !io.log && io.auto_reset && h->use_index &&
       lds_split + sizeof(Consts<T>) + 256 <= kLdsSplitMax) {

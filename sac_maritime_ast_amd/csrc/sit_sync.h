@@ -1,0 +1,435 @@
+// sit_sync.h — the step kernel with each ship's map predicates on a wave of their own, in the
+// same step (no speculation): synthetic-sampler rollouts with auto-reset (configs C3/C4).
+//
+// Included from sit_impl.h (inside its anonymous namespace, after sit_split.h).
+//
+// Forward Euler moves a ship with its pre-step velocities and heading (ship_model.py:632-643), so
+// the post-step position is known at the start of the step.  The D wave of each ship publishes it
+// (and the obstacle's IW of the step) before barrier A, then runs the sampler, guidance, control,
+// machinery and kinetics; meanwhile the ship's P wave evaluates the map predicates of that
+// position (boundary distance, hull in terrain, the IW test; MSRL_env_ex.py:490-542, 628-881).
+// Barrier B joins them: D decides the episode's end and runs the auto reset, P turns the distance
+// into the reward terms, and P0, one step behind, writes reward / done / status and the replay
+// transition.  Roles as in sit_split.h: 512-thread blocks of 2 env groups x {D0, D1, P0, P1},
+// mirrored in group 1 so each SIMD holds one D and one P wave.
+#pragma once
+
+template <typename T>
+struct SyncSlot {             // one step of the 64 envs of a group (ring of 2)
+  T pn[2][kWave], pe[2][kWave];   // post-step position per ship (D, before A)
+  T iwn[kWave], iwe[kWave];       // the obstacle's IW of the step (D1, before A)
+  T t[6][kWave];              // test ship: n, e, psi, rpm, |e_ct|, P_me (D0, before B)
+  T o[5][kWave];              // obstacle: n, e, psi, |e_ct|, SAC action (D1, before B)
+  uint32_t f[2][kWave];       // kSf* flags per ship (D, before B)
+  int32_t ep[kWave];          // episode step before the step (D1)
+  uint32_t pb[2][kWave];      // P per ship: bit 0 test terrain, bit 1 obstacle terrain, bit 2 IW terminal (before B)
+  T r_nto[kWave], r_o[kWave]; // P1 after B: the obstacle's reward terms
+  uint32_t bo[kWave];         // P1 after B: the obstacle's status bits | stop | done
+};
+template <typename T>
+struct SyncShared {
+  SyncSlot<T> d[2];
+};
+
+template <typename T>
+__host__ __device__ constexpr size_t sync_lds_bytes(size_t map_bytes) {
+  return ((map_bytes + 255) & ~size_t(255)) + 2 * ((sizeof(SyncShared<T>) + 255) & ~size_t(255));
+}
+
+// ------------------------------------------------------------------------------------------
+// D waves
+// ------------------------------------------------------------------------------------------
+template <typename T, int TYPE, int MACH>
+__device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, SyncShared<T>& X, int env, bool act) {
+#if SIT_SPLIT_CREF
+  const Consts<T>& c = cs;
+#else
+  const Consts<T> c = cs;
+#endif
+  const int lane = threadIdx.x & (kWave - 1);
+  const int n_env = a.n_env;
+  const int sid = TYPE * n_env + env;
+  const int n = a.io.n_steps;
+
+  Ship<T> s{};
+  Route<T> rt{};
+  T v_des = T(0);
+  T samp = T(0), eps = T(0), ppn = T(0), ppe = T(0), iwn = T(0), iwe = T(0);
+  int ep_step = 0;
+  uint32_t event = 0, episodes = 0;
+  double ab_len = 0.0, ab_alpha = 0.0, samp_limit = 0.0;
+  if (act) {
+    ep_step = a.st.ep_step[env];
+    load_ship(a.st, sid, s);
+    rt.nw = a.st.nw[sid];
+    rt.end_n = a.sc.end_n[sid];
+    rt.end_e = a.sc.end_e[sid];
+    v_des = init_val(a.sc, TYPE, SIT_INIT_DESIRED_SPEED, env, n_env);
+    rt.tn = a.st.wn + (size_t)TYPE * a.cap * n_env + env;
+    rt.te = a.st.we + (size_t)TYPE * a.cap * n_env + env;
+    rt.stride = n_env;
+    rt.load_leg(s.k);
+    if (TYPE == 1) {
+      samp = a.st.env[0][env]; eps = a.st.env[1][env];
+      ppn = a.st.env[2][env]; ppe = a.st.env[3][env];
+      iwn = a.st.env[4][env]; iwe = a.st.env[5][env];
+      event = a.st.event[env];
+      episodes = a.st.episodes[env];
+      ab_len = a.sc.ab_len[env];
+      ab_alpha = a.sc.ab_alpha[env];
+      samp_limit = ieee_mul(ab_len, cs.x.theta);   // MSRL_env_ex.py:569
+    }
+  }
+  T p0[6] = {};
+  int nw0 = 0;
+  typename Route<T>::Leg leg0{};
+  if (act) {
+    for (int j = 0; j < 6; ++j) p0[j] = init_val(a.sc, TYPE, SIT_INIT_NORTH + j, env, n_env);
+    nw0 = a.sc.nw0[sid];
+    Route<T> r0 = rt;
+    r0.nw = nw0;
+    r0.load_leg(1);
+    leg0 = r0.leg();
+  }
+  uint32_t uf = __builtin_amdgcn_readfirstlane((a.io.next_state ? 1u : 0u) | (a.io.action_out ? 16u : 0u) |
+                                               (c.collision_bias ? kUfCollBias : 0u) |
+                                               (c.sg_mode != SIT_SG_MOTOR ? kUfBlackout : 0u));
+  T* p_ns = (uf & 1) ? a.io.next_state + (size_t)env * SIT_OBS_DIM + (TYPE == 0 ? 0 : 6) : nullptr;
+  T* p_ao = (uf & 16) ? a.io.action_out + (size_t)env * 4 : nullptr;
+  const size_t row_step = (size_t)n_env;
+
+  for (int it = 0; it < n; ++it) {
+    asm volatile("" : "+s"(uf));
+    SyncSlot<T>& xd = X.d[it & 1];
+    T sp = T(0), cp = T(1);
+    T n1 = s.n, e1 = s.e;
+    bool sac = false;
+    double ang = 0.0, act_n = 0.0;
+    if (act) {
+      xsincos(s.psi, &sp, &cp);
+      if (TYPE == 0 || !s.stop) euler_position(c, s, sp, cp, n1, e1);
+      if (TYPE == 1) {
+        // synthetic AST sampler (uniform_policy.py:20-22 scaled by pi/6): the IW of
+        // this step is published with the position, for P1's IW test
+        sac = ep_step == 0 || ((double)samp >= ab_len && !s.stop);
+        if (sac) {
+          const double u01 = sampler_uniform(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
+          act_n = u01 * 2.0 - 1.0;
+          ang = act_n * (M_PI / 6.0);
+          iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
+          ++event;
+        }
+        xd.iwn[lane] = iwn; xd.iwe[lane] = iwe;
+      }
+      xd.pn[TYPE][lane] = n1; xd.pe[TYPE][lane] = e1;
+    }
+    __syncthreads();   // A: positions (and the IW) published
+    if (act) {
+      T o_rpm, o_ect, o_pme = T(0);
+      bool ect_over = false;
+      uint32_t fl = s.stop ? kSfStopPre : 0u;
+      if (TYPE == 1) {
+        const bool init_f = ep_step == 0;
+        if (sac) fl |= kSfSac;
+        if (s.stop) {                    // obs_step (MSRL_Env.py:287-402): stop path (Q10)
+          s.ticks += 2;
+          o_rpm = s.lrpm; o_ect = s.lect; o_pme = s.lpme;
+          ect_over = (double)o_ect > cs.x.e_tol;
+        } else {
+          if (sac) {                     // update_route: insert at index -1 (Q16)
+            if (!rt.insert(iwn, iwe, s.k, a.cap)) fl |= kSfOverflow;
+            samp = T(0);
+          }
+          const T pre_n = s.n, pre_e = s.e;
+          T rudder, thr, psi_ref;
+          guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+          o_rpm = s.w * c.rpm_k;
+          o_pme = power_me_kw(c, thr);
+          s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
+          ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
+          if (!init_f) {
+            const T dn = pre_n - ppn, de = pre_e - ppe;
+            const T d = xsqrt(dn * dn + de * de);
+            eps = eps + d;
+            samp = samp + d;
+          }
+          ppn = pre_n; ppe = pre_e;
+          s.ticks += 1;
+        }
+        const bool arrive = within_radius(s.n, s.e, rt.end_n, rt.end_e, c.arrive_d2_le);
+        const bool horizon = outside(c, s.n, s.e, c.half_len);
+        const bool nav = ect_over || (double)samp > samp_limit;
+        fl |= (arrive ? kSfArrive : 0u) | (horizon ? kSfHorizon : 0u) | (nav ? kSfNav : 0u) |
+              ((horizon || nav) ? kSfDoneNt : 0u);
+        if (arrive || horizon || nav) s.stop = 1;
+        xd.o[0][lane] = s.n; xd.o[1][lane] = s.e; xd.o[2][lane] = s.psi; xd.o[3][lane] = o_ect;
+        xd.o[4][lane] = (T)act_n;
+        xd.f[1][lane] = fl;
+        xd.ep[lane] = ep_step;
+        if (uf & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_ect); }
+        if (uf & 16) { store2(p_ao, iwn, iwe); store2(p_ao + 2, angle_or_nan(sac, (T)ang), sac ? T(1) : T(0)); }
+      } else {
+        // test_step (MSRL_Env.py:219-285)
+        T rudder, thr, psi_ref;
+        const T i1_0 = s.i1, i2_0 = s.i2;
+        guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+        if (uf & kUfCollBias) {          // is_collision_imminent() on all-zero states (Q1)
+          thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
+          rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
+        }
+        o_rpm = s.w * c.rpm_k;
+        o_pme = power_me_kw(c, thr);
+        const bool mech = rpm_fails<T, MACH>(c, cs.x, s.w, o_rpm);
+        bool blk = false;
+        if (uf & kUfBlackout) {
+          blk = o_pme > c.blackout_kw;
+          if (!kIsF32<T> || xabs(o_pme - c.blackout_kw) <= T(1e-4) * (xabs(o_pme) + T(1)))
+            blk = power_me_kw_exact(c.sg_mode, cs.x, throttle_exact(cs.x, s.u, v_des, i1_0, i2_0,
+                                                                    c.collision_bias != 0, MACH == 1))
+                  > cs.x.blackout;
+        }
+        s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
+        ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
+        s.ticks += 1;
+        const bool arrive = within_radius(s.n, s.e, rt.end_n, rt.end_e, c.arrive_d2_le);
+        const bool horizon = outside(c, s.n, s.e, c.half_len);
+        const bool any = arrive || horizon || mech || ect_over || blk;
+        fl |= (arrive ? kSfArrive : 0u) | (horizon ? kSfHorizon : 0u) | (mech ? kSfMech : 0u) |
+              (ect_over ? kSfEct : 0u) | (blk ? kSfBlk : 0u) | (any ? kSfDoneNt : 0u);
+        if (any) s.stop = 1;
+        xd.t[0][lane] = s.n; xd.t[1][lane] = s.e; xd.t[2][lane] = s.psi;
+        xd.t[3][lane] = o_rpm; xd.t[4][lane] = o_ect; xd.t[5][lane] = o_pme;
+        xd.f[0][lane] = fl;
+        if (uf & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_rpm); store2(p_ns + 4, o_ect, o_pme); }
+      }
+    }
+    __syncthreads();   // B: both ships' step and their map predicates
+    // the episode's end (every predicate, the collision) and the auto reset (main_ast.py:314-333)
+    if (act) {
+      const T tn = xd.t[0][lane], te = xd.t[1][lane], on = xd.o[0][lane], oe = xd.o[1][lane];
+      const bool coll = closer_than(tn, te, on, oe, c.coll_d2);
+      const bool env_done = ((xd.f[0][lane] | xd.f[1][lane]) & kSfDoneNt) || ((xd.pb[0][lane] | xd.pb[1][lane]) & 7u) ||
+                            coll;
+      if (coll) s.stop = 1;
+      if (TYPE == 1 && (xd.pb[1][lane] & 4u)) s.stop = 1;   // the IW terminal stops the obstacle (Q11)
+      rt.fixup(s.k);
+      ep_step += 1;
+      if (env_done) {
+        // reset() (MSRL_Env.py:147-188; shaft speed and every PI/PID integrator persist, Q6) + init_step()
+        s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];
+        s.ect_int = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
+        rt.nw = nw0;
+        rt.set_leg(leg0);
+        ep_step = 0;
+        if (TYPE == 1) { samp = T(0); eps = T(0); ++episodes; }
+        init_step_ship(c, cs.x, s, rt, v_des);
+      }
+    }
+    p_ns += row_step * SIT_OBS_DIM;
+    p_ao += row_step * 4;
+  }
+  __syncthreads();   // C: P1's reward terms of the last step (P0 writes that step's outputs)
+  if (act) {
+    store_ship(a.st, sid, s);
+    a.st.nw[sid] = rt.nw;
+    if (TYPE == 1) {
+      a.st.env[0][env] = samp; a.st.env[1][env] = eps;
+      a.st.env[2][env] = ppn; a.st.env[3][env] = ppe;
+      a.st.env[4][env] = iwn; a.st.env[5][env] = iwe;
+      a.st.ep_step[env] = ep_step;
+      a.st.event[env] = event;
+      a.st.episodes[env] = episodes;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// P waves
+// ------------------------------------------------------------------------------------------
+template <typename T, int TYPE>
+__device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, const Map<T>& map_in,
+                                      SyncShared<T>& X, int env, bool act) {
+  const Consts<T> c = cs;
+  Map<T> map = map_in;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int n_env = a.n_env;
+  const int n = a.io.n_steps;
+  T iw_tn = T(0), iw_te = T(0);     // P1: the IW test's cache (the IW changes at sampling events)
+  bool iw_valid = false, iw_in = false;
+  T lo[SIT_OBS_DIM] = {};           // P0: the observation before the step (replay transition)
+  if (TYPE == 0 && act)
+    for (int j = 0; j < SIT_OBS_DIM; ++j) lo[j] = a.st.last_obs[(size_t)j * n_env + env];
+  T r_nt_t = T(0), r_term_t = T(0); // P0: the test ship's reward terms and bits of the last step
+  uint32_t bits_t = 0;
+  T dobst = T(0);
+  bool terrain = false, iw_term = false;
+  uint32_t uf = __builtin_amdgcn_readfirstlane((a.io.reward ? 2u : 0u) | (a.io.done ? 4u : 0u) |
+                                               (a.io.status ? 8u : 0u) | (a.io.transitions ? kUfTrans : 0u) |
+                                               (a.io.done_count ? kUfDoneCnt : 0u) |
+                                               (a.io.mask_horizon > 0 ? kUfMaskH : 0u));
+
+  // P0: reward, done, status, replay transition and done count of step j (MSRL_env_ex.py:906-980)
+  auto outputs = [&](int j) {
+    const SyncSlot<T>& xd = X.d[j & 1];
+    bool env_done = false;
+    if (act) {
+      const T tn = xd.t[0][lane], te = xd.t[1][lane], on = xd.o[0][lane], oe = xd.o[1][lane];
+      const bool coll = closer_than(tn, te, on, oe, c.coll_d2);
+      const uint32_t bo = xd.bo[lane];
+      env_done = (bits_t & SIT_ST_TEST_DONE) || (bo & kDoneBit) || coll;
+      const T dn = tn - on, de = te - oe;
+      const T r_snt = (bo & kStopBit) ? T(0) : (T(1) - xsqrt(dn * dn + de * de) * c.inv_maxn) * T(0.001);
+      const T rs = coll ? T(2000) : T(0);
+      const T reward = r_nt_t + r_term_t + xd.r_nto[lane] + xd.r_o[lane] + r_snt + rs;
+      const uint32_t status = ((bits_t | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
+      const size_t row = (size_t)j * n_env + env;
+      if (uf & 2) a.io.reward[row] = reward;
+      if (uf & 4) a.io.done[row] = env_done ? 1 : 0;
+      if (uf & 8) a.io.status[row] = status;
+      const bool sac = (xd.f[1][lane] & kSfSac) != 0;
+      if (uf & kUfTrans) {             // replay transition of a sampling event (main_ast.py:385-396)
+        const unsigned long long m = __ballot(sac);
+        if (m) {
+          const int lead = __builtin_ctzll(m);
+          int base = 0;
+          if (lane == lead) base = atomicAdd(a.io.transition_count, (int)__popcll(m));
+          base = __shfl(base, lead);
+          const int slot = base + (int)__popcll(m & ((1ull << lane) - 1ull));
+          if (sac && slot < a.io.transition_capacity) {
+            T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
+            for (int q = 0; q < SIT_OBS_DIM; ++q) rec[q] = lo[q];
+            rec[10] = xd.o[4][lane];
+            rec[11] = reward;
+            for (int q = 0; q < 6; ++q) rec[12 + q] = xd.t[q][lane];
+            for (int q = 0; q < 4; ++q) rec[18 + q] = xd.o[q][lane];
+            const bool horizon_hit = (uf & kUfMaskH) && xd.ep[lane] + 2 == a.io.mask_horizon;
+            rec[22] = (horizon_hit || !env_done) ? T(1) : T(0);
+            rec[23] = (T)(a.io.env_id_offset + env);
+          }
+        }
+      }
+      // (the LDS values read unconditionally, the initial observation in its own rare branch: a
+      // select between the two sources became generic-pointer loads)
+      for (int q = 0; q < 6; ++q) lo[q] = xd.t[q][lane];
+      for (int q = 0; q < 4; ++q) lo[6 + q] = xd.o[q][lane];
+      if (env_done)
+        for (int q = 0; q < SIT_OBS_DIM; ++q) lo[q] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + q];
+    }
+    if (uf & kUfDoneCnt) {
+      const unsigned long long m = __ballot(env_done);
+      if (lane == 0 && m) atomicAdd(a.io.done_count + j, (int)__popcll(m));
+    }
+  };
+
+  for (int it = 0; it < n; ++it) {
+    asm volatile("" : "+s"(uf));
+    asm volatile("" : "+s"(map.use_index), "+s"(map.use_cells), "+s"(map.n_edge), "+s"(map.n_poly));
+    SyncSlot<T>& xd = X.d[it & 1];
+    __syncthreads();   // A: this step's positions
+    if (TYPE == 0 && it >= 1) outputs(it - 1);
+    // the map predicates of the post-step position (MSRL_env_ex.py:490-542, 628-881)
+    if (act) {
+      const T sn = xd.pn[TYPE][lane], se = xd.pe[TYPE][lane];
+      DistPf<T> pf;
+      pf_cell(c, map, sn, se, pf);
+      pf_edges(map, pf);
+      dobst = pf_finish(map, pf, sn, se);
+      terrain = hull_in_terrain_cls(c, map, sn, se, dobst, pf.cls, pf.cell_f, pf.word_f);
+      if (TYPE == 1) {
+        const T wn = xd.iwn[lane], we = xd.iwe[lane];
+        if (!iw_valid || wn != iw_tn || we != iw_te) {
+          iw_in = pip_point(c, map, wn, we);
+          iw_tn = wn; iw_te = we; iw_valid = true;
+        }
+        iw_term = outside(c, wn, we, T(0)) || iw_in;   // Q11
+        xd.pb[1][lane] = (terrain ? 2u : 0u) | (iw_term ? 4u : 0u);
+      } else {
+        xd.pb[0][lane] = terrain ? 1u : 0u;
+      }
+    }
+    __syncthreads();   // B: the D waves' step results
+    if (act) {
+      const uint32_t fl = xd.f[TYPE][lane];
+      int stop = (fl & kSfStopPre) ? 1 : 0;
+      bool done = false;
+      T r_nt = T(0), r_term = T(0);
+      uint32_t bits = 0;
+      if (TYPE == 0) {
+        r_nt = xabs(xd.t[4][lane]) * c.inv_e_tol + (T(1) - dobst * c.inv_maxn) * T(0.01);
+        const bool pred[6] = {(fl & kSfArrive) != 0, (fl & kSfHorizon) != 0, terrain, (fl & kSfMech) != 0,
+                              (fl & kSfEct) != 0, (fl & kSfBlk) != 0};
+        const T rew[6] = {T(0), T(0), T(1000), T(1000), T(1000), T(1000)};
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          if (pred[i]) {
+            if (!stop) r_term = r_term + rew[i];
+            stop = 1;
+            done = true;
+            bits |= 1u << i;
+          }
+        }
+        if (done) bits |= SIT_ST_TEST_DONE;
+        r_nt_t = r_nt; r_term_t = r_term; bits_t = bits;
+      } else {
+        if (!stop)
+          r_nt = T(0.1) - xabs(xd.o[3][lane]) * c.inv_e_tol * T(0.01) - (T(1) - dobst * c.inv_maxn) * T(0.01);
+        bits = (fl & kSfOverflow) ? SIT_ST_ROUTE_OVERFLOW : 0u;
+        if (fl & kSfArrive) { stop = 1; bits |= SIT_ST_OBS_ENDPOINT; }
+        if (fl & kSfHorizon) { stop = 1; done = true; bits |= SIT_ST_OBS_HORIZON; }
+        if (terrain) {                   // done without stop flag (Q12)
+          if (!stop) r_term = r_term - T(1000);
+          done = true;
+          bits |= SIT_ST_OBS_TERRAIN;
+        }
+        if (iw_term) {
+          if (!stop) r_term = r_term - T(1000);
+          stop = 1; done = true;
+          bits |= SIT_ST_OBS_IW_TERMINAL;
+        }
+        if (fl & kSfNav) {
+          if (!stop) r_term = r_term - T(1000);
+          stop = 1; done = true;
+          bits |= SIT_ST_OBS_NAVIGATION;
+        }
+        if (done) bits |= SIT_ST_OBS_DONE;
+        xd.r_nto[lane] = r_nt;
+        xd.r_o[lane] = r_term;
+        xd.bo[lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u);
+      }
+    }
+  }
+  __syncthreads();   // C
+  if (TYPE == 0) {
+    if (n >= 1) outputs(n - 1);
+    if (act)
+      for (int j = 0; j < SIT_OBS_DIM; ++j) a.st.last_obs[(size_t)j * n_env + env] = lo[j];
+  }
+}
+
+template <typename T, int MACH>
+__global__ __launch_bounds__(512) void k_env_steps_sync(const KArgs<T> a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ Consts<T> cs;
+  for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
+    reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
+  const Map<T> map = stage_map(a, smem);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int group = w >> 2;
+  const int role = group == 0 ? (w & 3) : ((w & 3) ^ 2);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int env = (blockIdx.x * 2 + group) * kWave + lane;
+  const bool act = env < a.n_env;
+  SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(
+      smem + (((size_t)a.map_bytes + 255) & ~size_t(255)) +
+      (size_t)group * ((sizeof(SyncShared<T>) + 255) & ~size_t(255)));
+  __syncthreads();   // constants copied, map staged
+#ifndef SIT_SYNC_PRIO
+#define SIT_SYNC_PRIO 0
+#endif
+  if (SIT_SYNC_PRIO == 1 && role < 2) __builtin_amdgcn_s_setprio(1);        // D waves first
+  if (SIT_SYNC_PRIO == 2 && role == 1) __builtin_amdgcn_s_setprio(1);       // the obstacle's D wave first
+  if (role == 0) sync_d<T, 0, MACH>(a, cs, X, env, act);
+  else if (role == 1) sync_d<T, 1, MACH>(a, cs, X, env, act);
+  else if (role == 2) sync_p<T, 0>(a, cs, map, X, env, act);
+  else sync_p<T, 1>(a, cs, map, X, env, act);
+}

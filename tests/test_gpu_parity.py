@@ -607,10 +607,7 @@ def test_device_transcendentals_vs_reference_libm(fast_tu):
 # the pipelined kernel (sit_split.h) against the one-wave-per-ship kernel
 # ------------------------------------------------------------------------------------------
 def _rollouts(env, blob, kernel, launches, steps, monkeypatch):
-    if kernel == "pipelined":
-        monkeypatch.setenv("SIT_STEP_KERNEL", "pipelined")
-    else:
-        monkeypatch.delenv("SIT_STEP_KERNEL", raising=False)
+    monkeypatch.setenv("SIT_STEP_KERNEL", kernel)
     env.load_state_blob(blob)
     res = []
     for i in range(launches):
@@ -624,8 +621,9 @@ def _rollouts(env, blob, kernel, launches, steps, monkeypatch):
     return res, st
 
 
+@pytest.mark.parametrize("kernel", ["pipelined", "sync"])
 @pytest.mark.parametrize("precision", [64, 32])
-def test_pipelined_kernel_equals_classic(precision, monkeypatch):
+def test_pipelined_kernel_equals_classic(precision, kernel, monkeypatch):
     """The speculative two-wave-per-ship kernel (synthetic sampler, auto-reset: the C3 workload)
     against k_env_steps from the same state (after a 600-step warm-up, so episodes are
     desynchronised) on 2000 envs (a partial last block).  float64: 3 launches x 700 steps with the
@@ -643,7 +641,7 @@ def test_pipelined_kernel_equals_classic(precision, monkeypatch):
     env.rollout(600, seed=40)
     blob = env.state_blob()
     a, sa = _rollouts(env, blob, "classic", launches, steps, monkeypatch)
-    b, sb = _rollouts(env, blob, "pipelined", launches, steps, monkeypatch)
+    b, sb = _rollouts(env, blob, kernel, launches, steps, monkeypatch)
     tol = TOL64 if precision == 64 else 1e-3
     n_terr, worst = 0, 0.0
     bitwise = True
@@ -664,5 +662,5 @@ def test_pipelined_kernel_equals_classic(precision, monkeypatch):
     for k in so.SHIP_REAL:
         err = rel_err(sb[k], sa[k], SCALE[k]).max()
         assert err <= tol, f"final state {k} rel err {err:.3e}"
-    print(f"pipelined vs classic f{precision}: {n_terr} terrain/IW terminations (redone steps), bitwise {bitwise}, worst rel err {worst:.2e}")
+    print(f"{kernel} vs classic f{precision}: {n_terr} terrain/IW terminations (redone steps), bitwise {bitwise}, worst rel err {worst:.2e}")
     assert n_terr > 0 or precision == 32, "the case exercises no redone step"
