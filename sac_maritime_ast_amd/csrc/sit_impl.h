@@ -1388,9 +1388,10 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
       HIP_TRY(h, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sync));
       h->lds_attr_sync[mach] = (int)lds_sync;
     }
-    const int blocks2 = (h->n_env + 2 * kWave - 1) / (2 * kWave);
-    if (mach) hipLaunchKernelGGL((k_env_steps_sync<T, 1>), dim3(blocks2), dim3(512), lds_sync, stream, a);
-    else hipLaunchKernelGGL((k_env_steps_sync<T, 0>), dim3(blocks2), dim3(512), lds_sync, stream, a);
+    const int gs = kSyncGroups;
+    const int blocks2 = (h->n_env + gs * kWave - 1) / (gs * kWave);
+    if (mach) hipLaunchKernelGGL((k_env_steps_sync<T, 1>), dim3(blocks2), dim3(256 * gs), lds_sync, stream, a);
+    else hipLaunchKernelGGL((k_env_steps_sync<T, 0>), dim3(blocks2), dim3(256 * gs), lds_sync, stream, a);
     HIP_TRY(h, hipGetLastError());
     return SIT_OK;
   }

@@ -14,6 +14,12 @@
 // mirrored in group 1 so each SIMD holds one D and one P wave.
 #pragma once
 
+#ifndef SIT_SYNC_GROUPS
+#define SIT_SYNC_GROUPS 1   // env groups per block: 1 = 256-thread blocks, two per CU, role order by block parity
+                            // (2 groups in 512-thread blocks measured 8 % slower: barriers couple the groups)
+#endif
+#define SIT_SYNC_GROUPS_LDS SIT_SYNC_GROUPS
+
 template <typename T>
 struct SyncSlot {             // one step of the 64 envs of a group (ring of 2)
   T pn[2][kWave], pe[2][kWave];   // post-step position per ship (D, before A)
@@ -33,7 +39,7 @@ struct SyncShared {
 
 template <typename T>
 __host__ __device__ constexpr size_t sync_lds_bytes(size_t map_bytes) {
-  return ((map_bytes + 255) & ~size_t(255)) + 2 * ((sizeof(SyncShared<T>) + 255) & ~size_t(255));
+  return ((map_bytes + 255) & ~size_t(255)) + SIT_SYNC_GROUPS_LDS * ((sizeof(SyncShared<T>) + 255) & ~size_t(255));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -406,8 +412,10 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   }
 }
 
+constexpr int kSyncGroups = SIT_SYNC_GROUPS;
+
 template <typename T, int MACH>
-__global__ __launch_bounds__(512) void k_env_steps_sync(const KArgs<T> a) {
+__global__ __launch_bounds__(128 * kSyncGroups * 2) void k_env_steps_sync(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Consts<T> cs;
   for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
@@ -415,9 +423,10 @@ __global__ __launch_bounds__(512) void k_env_steps_sync(const KArgs<T> a) {
   const Map<T> map = stage_map(a, smem);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int group = w >> 2;
-  const int role = group == 0 ? (w & 3) : ((w & 3) ^ 2);
+  const int flip = kSyncGroups == 1 ? (int)(blockIdx.x & 1) : group;
+  const int role = flip == 0 ? (w & 3) : ((w & 3) ^ 2);
   const int lane = threadIdx.x & (kWave - 1);
-  const int env = (blockIdx.x * 2 + group) * kWave + lane;
+  const int env = (blockIdx.x * kSyncGroups + group) * kWave + lane;
   const bool act = env < a.n_env;
   SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(
       smem + (((size_t)a.map_bytes + 255) & ~size_t(255)) +
