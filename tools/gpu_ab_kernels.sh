@@ -1,6 +1,6 @@
 #!/bin/bash
-# Selected GPU tests (one process), then the default bench with the pipelined and the classic step
-# kernel:   [K=<pytest -k expr>] tools/gpu_ab_kernels.sh "<test paths>" [bench args]
+# Selected GPU tests (one process), then the default bench with each step kernel (sync = the default
+# two-wave kernel, classic = k_env_steps, pipelined = the speculative split):   [K=<pytest -k expr>] tools/gpu_ab_kernels.sh "<test paths>" [bench args]
 set -u
 mkdir -p gpurun_out
 T=${1:-tests}
@@ -11,8 +11,8 @@ rc=$?
 echo "pytest rc=$rc"
 grep -E "PASSED|FAILED|ERROR|passed|failed|Error|pipelined vs|assert" gpurun_out/ab_tests.log | tail -40
 if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then exit $rc; fi
-for kern in pipelined classic; do
-  if [ $kern = pipelined ]; then export SIT_STEP_KERNEL=pipelined; else unset SIT_STEP_KERNEL; fi
+for kern in sync classic pipelined; do
+  export SIT_STEP_KERNEL=$kern
   timeout -k 10 300 python -u bench.py --no-cpu-baseline "$@" > gpurun_out/ab_$kern.json 2> gpurun_out/ab_$kern.err
   brc=$?
   echo "bench $kern rc=$brc"
