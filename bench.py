@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--transitions", action="store_true",
                     help="N = 1: write the replay transitions too (every rank writes them at N > 1)")
     ap.add_argument("--launch-trace", action="store_true", help="print every launch's kernel ms to stderr")
+    ap.add_argument("--no-c5", action="store_true", help="rollout mode: skip the config C5 (policy) line")
+    ap.add_argument("--c5-steps", type=int, default=32 * 16 * 16, help="timed steps of the C5 line")
+    ap.add_argument("--c5-warmup", type=int, default=32 * 16 * 60, help="warm-up steps of the C5 line")
     args = ap.parse_args()
     if args.chunk is None:
         args.chunk = 32 if args.mode == "policy" else 40000
@@ -292,12 +295,17 @@ def dry_run(args, rank, world, dev):
             "gathered": g.gathered, "dropped": g.dropped(), "records_per_launch_ok": got == want if rank == 0 else None}
 
 
-def roofline(alg_bytes, kern_ms, pmc):
+def roofline(alg_bytes, kern_ms, pmc, kernel):
+    """kernel: the instantiation the timed launches ran (sit_step_kernel of the handle)."""
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": (pmc["hbm_bytes_per_launch"] if pmc else None),
-            "kernel": "k_env_steps", "kernel_ms_per_launch": kern_ms,
+            "kernel": kernel, "kernel_ms_per_launch": kern_ms,
             "algorithmic_bytes_per_launch": alg_bytes}
+
+
+def kernel_name(env):
+    return env.lib.sit_step_kernel(env.handle).decode()
 
 
 # VALU issue peak of the chip: 256 CUs x 4 SIMD-32 x one wave64 VALU instruction per 2 cycles at
@@ -317,8 +325,7 @@ def roofline_valu(kern_ms, pmc, n_env, chunk):
     inst = per * waves * chunk
     achieved = inst / (kern_ms * 1e-3)
     return {"bound": "valu-issue", "achieved": achieved, "peak": VALU_PEAK_INST_S, "unit": "wave-instr/s",
-            "frac": achieved / VALU_PEAK_INST_S, "valu_per_wave_step": per,
-            "one_wave_per_simd_ceiling_frac": 0.5,
+            "frac": achieved / VALU_PEAK_INST_S, "valu_per_wave_step": per, "waves": waves,
             "source": pmc.get("source")}
 
 
@@ -417,13 +424,18 @@ def bench_rollout(args, rank, world, dev):
                                        float(st["n_wpt"][0].double().mean().item()), args.mode)
     env_steps = world * n_env * steps
     pmc = latest_pmc(args.precision, args.mode, n_env, chunk)
-    rl = roofline(alg, kern_ms, pmc)
+    rl = roofline(alg, kern_ms, pmc, kernel_name(env))
     rl["algorithmic_bytes_per_env_step"] = alg / (n_env * chunk)
     rl["launch_ms"] = stats_of(launch_ms)
     rl["kernel_ms_statistic"] = "median over the timed launches (HIP events on the launch stream)"
-    workload = ("C3: 65 536 ships = 32 768 two-ship envs per GPU, random IW actions, auto-reset" if world == 1 else
-                f"C4: {2 * n_env * world} ships sharded over {world} GPUs, random IW actions, RCCL gather of the "
-                f"replay transitions to the learner")
+    if args.mode == "step":
+        workload = (f"drop-in sit_step: one MultiShipRLEnv.step launch per env step for {n_env} envs "
+                    f"({2 * n_env} ships), explicit IW actions, no auto-reset")
+    elif world == 1:
+        workload = "C3: 65 536 ships = 32 768 two-ship envs per GPU, random IW actions, auto-reset"
+    else:
+        workload = (f"C4: {2 * n_env * world} ships sharded over {world} GPUs, random IW actions, RCCL gather of "
+                    f"the replay transitions to the learner")
     res = {
         "value": env_steps / elapsed, "steps": steps, "warmup": warm, "ms_per_step": elapsed * 1e3 / steps,
         "config": {"workload": workload, "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env,
@@ -450,13 +462,19 @@ def bench_rollout(args, rank, world, dev):
 def bench_policy(args, rank, world, dev):
     """Config C5: the SAC-AST Gaussian policy (fp32 actor, 256x256 MLP, one HIP kernel) chooses the
     IWs; envs split into `--groups` groups on separate HIP streams so one group's actor runs while
-    the others' env kernels run.  value = env-steps executed (device counter) / time."""
+    the others' env kernels run.  value = env-steps executed (device counter) / time.  At N > 1
+    every group's replay transitions (all launches of a HIP graph append to one buffer) go to the
+    learner (rank 0) over RCCL after each graph replay, pipelined behind the next replay."""
     from sac_maritime_ast_amd import VecMultiShipRLEnv, make_scenario
-    from sac_maritime_ast_amd.samplers import GaussianPolicy, PolicySampler
-    from sac_maritime_ast_amd.shard import shard_offset
+    from sac_maritime_ast_amd.samplers import GaussianPolicy, OverlappedPolicySampler, PolicySampler
+    from sac_maritime_ast_amd.shard import AsyncTransitionGather, shard_offset
 
     n_env, G, chunk = args.n_env, args.groups, args.chunk
     per = n_env // G
+    per_graph = max(2, min(args.graph_launches, max(2, args.steps // chunk)) // 2 * 2)   # even: 2-slot counter
+    gathering = world > 1 and not args.no_gather
+    # transitions of one graph replay per group: 1 per ~390 env-steps measured (C3), 1 per 96 here
+    tcap = per * chunk * per_graph // 96 if (gathering or args.transitions) else 0
     torch.manual_seed(args.seed)
     policy = GaussianPolicy(hidden=(256, 256)).to(dev)
     samplers = []
@@ -467,39 +485,52 @@ def bench_policy(args, rank, world, dev):
         env.reset()
         env.init_step()
         samplers.append(PolicySampler(env, policy, chunk=chunk, seed=args.seed, env_id_offset=off,
-                                      request_capacity=max(256, per // args.request_div)))
-    from sac_maritime_ast_amd.samplers import OverlappedPolicySampler
-    runner = OverlappedPolicySampler(samplers) if G > 1 else samplers[0]
+                                      request_capacity=max(256, per // args.request_div), transition_capacity=tcap))
+    runner = OverlappedPolicySampler(samplers) if G > 1 else None
     cur = torch.cuda.current_stream(dev)
-    # kernel duration of the env launches (eager, HIP events on each group's stream)
+    # kernel duration of the env launches: eager launches through the sampler (HIP events on each
+    # group's stream around the env kernel)
+    n_ev = 8
     ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
-          for _ in range(8)]
-    for i in range(8):
-        for g, sm in enumerate(samplers):
-            st = runner.streams[g] if G > 1 else cur
-            st.wait_stream(cur)
-            with torch.cuda.stream(st):
-                sm.io["request_count"].zero_()
-                ev[i][g][0].record(st)
-                sm.env.rollout(chunk, seed=args.seed, env_id_offset=sm.env_id_offset, out=sm.out, policy_io=sm.io)
-                ev[i][g][1].record(st)
-                sm.act()
-            cur.wait_stream(st)
+          for _ in range(n_ev)]
+    for i in range(n_ev):
+        if runner:
+            runner.launch(events=ev[i])
+        else:
+            samplers[0].launch(events=ev[i][0])
     torch.cuda.synchronize(dev)
     launch_ms = [a.elapsed_time(b) for row in ev for a, b in row]
+    kern = kernel_name(samplers[0].env)
     # the timed loop: HIP-graph replays of `per_graph` launches of every group
-    per_graph = max(2, min(args.graph_launches, args.steps // chunk) // 2 * 2)   # even: 2-slot request counter
-    runner.capture(per_graph)
-    n_rep = max(1, args.steps // (chunk * per_graph))
+    (runner or samplers[0]).capture(per_graph)
+    n_rep = max(2, args.steps // (chunk * per_graph))
     n_warm = max(1, args.warmup // (chunk * per_graph))
+    gathers = [AsyncTransitionGather(tcap, 24, samplers[0].env.dtype, dev, world) for _ in range(G)] if gathering else []
+    rep_no = [0]
+
+    def replay():
+        (runner or samplers[0]).replay()
+        i = rep_no[0]
+        for g, (sm, ga) in enumerate(zip(samplers, gathers)):
+            rec, cnt = ga.buffers(i)
+            rec.copy_(sm.out["transitions"])
+            cnt.copy_(sm.out["transition_count"])
+            ga.start(i)
+            ga.progress(i - 1)
+        rep_no[0] += 1
     for _ in range(n_warm):
-        runner.replay()
+        replay()
+    for ga in gathers:
+        ga.finish()
     torch.cuda.synchronize(dev)
+    g0 = [(ga.gathered, ga.dropped()) for ga in gathers]
     before = sum(int(sm.env_steps.item()) for sm in samplers)
 
     def run():
         for _ in range(n_rep):
-            runner.replay()
+            replay()
+        for ga in gathers:
+            ga.finish()
     elapsed = timed(dev, world, run)
     n_launch = n_rep * per_graph
     done_steps = sum(int(sm.env_steps.item()) for sm in samplers) - before
@@ -511,24 +542,30 @@ def bench_policy(args, rank, world, dev):
     rs = 4 if args.precision == 32 else 8
     alg = algorithmic_bytes_per_launch(per, chunk, rs, 3.0, 5.0, "rollout")
     pmc = latest_pmc(args.precision, "policy", per, chunk)
-    rl = roofline(alg, kern_ms, pmc)
+    rl = roofline(alg, kern_ms, pmc, kern)
     rl["launch_ms"] = stats_of(launch_ms)
     rl["note"] = "per group launch (n_env / groups envs), groups run concurrently on separate streams"
-    rl["kernel_ms_statistic"] = "median over 16 eager launches (HIP events on each group's stream)"
-    return {
-        "value": env_steps / elapsed, "steps": n_launch * chunk, "warmup": n_warm * per_graph * chunk,
-        "ms_per_step": elapsed * 1e3 / (n_launch * chunk),
-        "config": {"workload": "C5: 65 536 ships driven by the SAC-AST Gaussian policy (256x256 MLP, fp32, "
-                               "fused into one HIP actor kernel) interleaved with the HIP env step on "
-                               "separate streams",
-                   "actor": "sit_policy_actor (fused)" if all(sm.fused for sm in samplers) else "PyTorch-ROCm",
-                   "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env, "fused_steps_per_launch": chunk,
-                   "mode": "policy", "stream_groups": G, "launches_per_hip_graph": per_graph,
-                   "parallelism": f"env-shard x{world}",
-                   "env_step_fraction": env_steps / (world * n_env * n_launch * chunk),
-                   "policy_evaluations": int(sum(int(sm.served.item()) for sm in samplers))},
-        "roofline": rl,
-    }
+    rl["kernel_ms_statistic"] = f"median over {n_ev * G} eager launches (HIP events on each group's stream)"
+    cfg = {"workload": "C5: 65 536 ships driven by the SAC-AST Gaussian policy (256x256 MLP, fp32, "
+                       "fused into one HIP actor kernel) interleaved with the HIP env step on "
+                       "separate streams" if world == 1 else
+                       f"C5 x{world}: {2 * n_env * world} policy-driven ships sharded over {world} GPUs",
+           "actor": "sit_policy_actor (fused)" if all(sm.fused for sm in samplers) else "PyTorch-ROCm",
+           "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env, "fused_steps_per_launch": chunk,
+           "mode": "policy", "stream_groups": G, "launches_per_hip_graph": per_graph,
+           "parallelism": f"env-shard x{world}",
+           "env_step_fraction": env_steps / (world * n_env * n_launch * chunk),
+           "policy_evaluations": int(sum(int(sm.served.item()) for sm in samplers))}
+    if gathers:
+        stats = torch.tensor([sum(ga.gathered for ga in gathers) - sum(x[0] for x in g0),
+                              sum(ga.dropped() for ga in gathers) - sum(x[1] for x in g0)],
+                             dtype=torch.float64, device=dev)
+        cfg["rccl_transition_gather"] = {
+            "to": "rank 0 (learner)", "records_gathered": int(stats[0].item()), "records_dropped": int(stats[1].item()),
+            "capacity_per_group_replay": tcap, "pipelining": "per group: count all-gather behind each graph replay; "
+                                                            "valid records point-to-point once the next replay is enqueued"}
+    return {"value": env_steps / elapsed, "steps": n_launch * chunk, "warmup": n_warm * per_graph * chunk,
+            "ms_per_step": elapsed * 1e3 / (n_launch * chunk), "config": cfg, "roofline": rl}
 
 
 def main():
@@ -544,6 +581,13 @@ def main():
             torch.distributed.destroy_process_group()
         return
     r = bench_policy(args, rank, world, dev) if args.mode == "policy" else bench_rollout(args, rank, world, dev)
+    c5 = None
+    if args.mode == "rollout" and not args.no_c5:
+        # config C5 beside the headline C3/C4 line: policy mode, driver-timed in the same run
+        a5 = argparse.Namespace(**vars(args))
+        a5.mode, a5.chunk = "policy", 32
+        a5.steps, a5.warmup = max(args.c5_steps, 32 * 16 * 2), args.c5_warmup
+        c5 = bench_policy(a5, rank, world, dev)
     result = {"metric": METRIC, "value": r["value"], "unit": "env-steps/s", "n_gpus": world, "steps": r["steps"],
               "warmup": r["warmup"], "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
               "vs_baseline": None, "dtype": "f32" if args.precision == 32 else "f64",
@@ -551,6 +595,10 @@ def main():
               "config": r["config"], "roofline": r["roofline"]}
     if r.get("roofline_valu"):
         result["roofline_valu"] = r["roofline_valu"]
+    if c5 is not None:
+        result["c5"] = {"metric": "env-steps/sec, 65 536 policy-driven ships per GPU (config C5)", "value": c5["value"],
+                        "unit": "env-steps/s", "steps": c5["steps"], "warmup": c5["warmup"],
+                        "ms_per_step": c5["ms_per_step"], "config": c5["config"], "roofline": c5["roofline"]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.seed, args.cpu_baseline_workers)
     if rank == 0:

@@ -233,6 +233,9 @@ const char* sit_last_error(const sit_handle* h);
 int32_t sit_abi_version(void);
 int32_t sit_precision(const sit_handle* h);
 int32_t sit_n_env(const sit_handle* h);
+/* Instantiation name of the step kernel the last sit_step / sit_rollout launch of `h` ran, e.g.
+ * "k_env_steps_sync<float,kSynth,MACH=0>" (diagnostics and bench labels; "" before the first). */
+const char* sit_step_kernel(const sit_handle* h);
 
 /* ---- setup (host pointers) --------------------------------------------------------- */
 /* Island map: PolygonObstacle(list_of_vertices_list) (obstacle.py:98-124).  Vertices are

@@ -275,7 +275,7 @@ __device__ __forceinline__ double angle_or_nan(bool has, double a) {
 //           sampling event without a fresh action waits for the rest of the launch and queues
 //           a request; the next launch consumes the action the policy wrote for it)
 // ---------------------------------------------------------------------------------------
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SPLIT)
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
 // Diagnostic builds only (tools/diag_paths.py): [type][0..15] predicate path statistics,
 // [type][16..23] shader-clock cycles per step phase (wave lane 0).
 __device__ unsigned long long g_sit_diag[2][32];
@@ -943,7 +943,6 @@ __global__ __launch_bounds__(128 * kGroups, SIT_MIN_WAVES) void k_env_steps(cons
   else env_steps<T, MODE, LDSMAP, LOG, 1, MACH>(a, smem, xs, cs);
 }
 
-#include "sit_split.h"
 #include "sit_sync.h"
 
 // MultiShipRLEnv.init_step for masked envs (one thread per ship)
@@ -1105,8 +1104,14 @@ struct sit_handle {
   int lds_attr[24] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
                       -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
-  int lds_attr_split[2] = {-1, -1};
-  int lds_attr_sync[2] = {-1, -1};    // the same for k_env_steps_sync
+  int lds_attr_sync[4] = {-1, -1, -1, -1};    // the same for k_env_steps_sync [mode policy][mach]
+  // step-kernel selection, read once at sit_create (diagnostics / A-B runs only):
+  //   SIT_STEP_KERNEL=classic  k_env_steps for every mode (default: k_env_steps_sync where it applies)
+  //   SIT_LDS_MAP=0|1          map read through the caches / staged in LDS for every launch
+  //                            (default: staged when the launch has >= kLdsMinSteps steps)
+  int kernel_classic = 0;
+  int lds_map_sel = -1;
+  char last_kernel[96] = {};         // the step kernel of the last sit_step / sit_rollout launch
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
   double fx0 = 0, fy0 = 0, finvx = 0, finvy = 0;
@@ -1336,24 +1341,71 @@ int ready(sit_handle* h) {
 // LDS budget of one step-kernel block: two blocks (4 waves, one per SIMD) must fit the CU's
 // 160 KB; above 80 KB only one block fits and the grid runs in two rounds (~1.75x slower)
 constexpr size_t kLdsBudget = 80 * 1024;
-constexpr size_t kLdsSplitMax = 160 * 1024;   // the CU's LDS: one block of the pipelined kernel per CU
+constexpr size_t kLdsCu = 160 * 1024;       // the CU's LDS (k_env_steps_sync: two 256-thread blocks per CU)
+// launches of fewer steps read the map through the caches instead of staging it into LDS: staging
+// 57 KB per block is a prologue that a single step (sit_step, the scalar drop-in) cannot amortise
+#ifndef SIT_LDS_MIN_STEPS
+#define SIT_LDS_MIN_STEPS 8
+#endif
+constexpr int kLdsMinSteps = SIT_LDS_MIN_STEPS;
 size_t map_lds_bytes(const sit_handle* h) { return (h->map_bytes + 255) & ~size_t(255); }
+
+// the step kernel of a launch as a readable instantiation name (sit_step_kernel)
+template <typename T>
+void set_kernel_name(sit_handle* h, bool sync, int mode, bool lds, bool log, int mach) {
+  static const char* const modes[3] = {"kExplicit", "kSynth", "kPolicy"};
+  const char* t = kIsF32<T> ? "float" : "double";
+  if (sync) snprintf(h->last_kernel, sizeof(h->last_kernel), "k_env_steps_sync<%s,%s,MACH=%d>", t, modes[mode], mach);
+  else snprintf(h->last_kernel, sizeof(h->last_kernel), "k_env_steps<%s,%s,%s,%s,MACH=%d>", t, modes[mode],
+                lds ? "map=LDS" : "map=global", log ? "log" : "nolog", mach);
+}
 
 template <typename T>
 int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   KArgs<T> a = make_args<T>(h);
   a.io = io;
-  const int blocks = (h->n_env + kEnvsPerBlock * kGroups - 1) / (kEnvsPerBlock * kGroups);
   const int mode = io.action_ne ? kExplicit : (io.policy_action ? kPolicy : kSynth);
-  // the map (edges, index, classes) is staged in LDS when it fits the budget next to the
-  // static exchange buffers; otherwise the predicates read it through the caches
+  const int mach = a.c.mach_simpl ? 1 : 0;
+  // k_env_steps_sync (sit_sync.h), two waves per ship with the map predicates on their own wave, for
+  // the rollouts with auto-reset whose actions come from the synthetic sampler (C3/C4: 1.75e10
+  // against 1.62e10 env-steps/s for k_env_steps) or from the policy (C5); k_env_steps for the
+  // explicit actions of sit_step, the trajectory log and rollouts without auto-reset
+  const size_t lds_sync = sync_lds_bytes<T>(h->map_bytes);
+  if (!h->kernel_classic && mode != kExplicit && !io.log && io.auto_reset && h->use_index &&
+      lds_sync + sizeof(Consts<T>) + 256 <= kLdsCu) {
+    const int slot = (mode == kPolicy ? 2 : 0) + mach;
+    const void* kern = mode == kPolicy ? (mach ? reinterpret_cast<const void*>(&k_env_steps_sync<T, kPolicy, 1>)
+                                               : reinterpret_cast<const void*>(&k_env_steps_sync<T, kPolicy, 0>))
+                                       : (mach ? reinterpret_cast<const void*>(&k_env_steps_sync<T, kSynth, 1>)
+                                               : reinterpret_cast<const void*>(&k_env_steps_sync<T, kSynth, 0>));
+    if (h->lds_attr_sync[slot] != (int)lds_sync) {
+      HIP_TRY(h, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sync));
+      h->lds_attr_sync[slot] = (int)lds_sync;
+    }
+    const int blocks = (h->n_env + kSyncLanes - 1) / kSyncLanes;
+    if (mode == kPolicy) {
+      if (mach) hipLaunchKernelGGL((k_env_steps_sync<T, kPolicy, 1>), dim3(blocks), dim3(256), lds_sync, stream, a);
+      else hipLaunchKernelGGL((k_env_steps_sync<T, kPolicy, 0>), dim3(blocks), dim3(256), lds_sync, stream, a);
+    } else {
+      if (mach) hipLaunchKernelGGL((k_env_steps_sync<T, kSynth, 1>), dim3(blocks), dim3(256), lds_sync, stream, a);
+      else hipLaunchKernelGGL((k_env_steps_sync<T, kSynth, 0>), dim3(blocks), dim3(256), lds_sync, stream, a);
+    }
+    HIP_TRY(h, hipGetLastError());
+    set_kernel_name<T>(h, true, mode, true, false, mach);
+    return SIT_OK;
+  }
+  const int blocks = (h->n_env + kEnvsPerBlock * kGroups - 1) / (kEnvsPerBlock * kGroups);
+  // the map (edges, index, classes) is staged in LDS when it fits the budget next to the static
+  // exchange buffers and the launch has enough steps to amortise the staging; otherwise the
+  // predicates read it through the caches
   const size_t stat = sizeof(Xchg<T>) * 2 * kGroups + sizeof(Consts<T>) + 256;
-  const bool lds_map = map_lds_bytes(h) + stat <= kLdsBudget;
+  const bool fits = map_lds_bytes(h) + stat <= kLdsBudget;
+  const bool lds_map = fits && (h->lds_map_sel == 1 || (h->lds_map_sel < 0 && io.n_steps >= kLdsMinSteps));
   const size_t lds = lds_map ? map_lds_bytes(h) : 0;
   auto go = [&](auto kern) -> int {
     // the dynamic-LDS attribute is set once per kernel and size (not per launch: launches may be
     // captured into HIP graphs)
-    const int slot = ((mode * 2 + (lds_map ? 1 : 0)) * 2 + (io.log ? 1 : 0)) * 2 + (a.c.mach_simpl ? 1 : 0);
+    const int slot = ((mode * 2 + (lds_map ? 1 : 0)) * 2 + (io.log ? 1 : 0)) * 2 + mach;
     if (lds_map && h->lds_attr[slot] != (int)lds) {
       HIP_TRY(h, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       h->lds_attr[slot] = (int)lds;
@@ -1367,57 +1419,16 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
     return lds_map ? go(k_env_steps<T, M, true, false, K>) : go(k_env_steps<T, M, false, false, K>);
   };
   auto pick = [&](auto mode_tag) -> int {
-    if (a.c.mach_simpl) return pick_mach(mode_tag, std::integral_constant<int, 1>{});
+    if (mach) return pick_mach(mode_tag, std::integral_constant<int, 1>{});
     return pick_mach(mode_tag, std::integral_constant<int, 0>{});
   };
-  // SIT_STEP_KERNEL=pipelined: the speculative two-waves-per-ship kernel (sit_split.h); measured
-  // slower than k_env_steps at C3 (1.47e10 vs 1.62e10 env-steps/s).
-  // Default for the synthetic sampler with auto-reset (the C3/C4 workload): k_env_steps_sync
-  // (sit_sync.h), two waves per ship with the map predicates on their own wave (C3: 1.75e10
-  // against 1.62e10 env-steps/s for k_env_steps).
-  // SIT_STEP_KERNEL=classic selects k_env_steps, =pipelined the speculative kernel of sit_split.h.
-  const char* sel = getenv("SIT_STEP_KERNEL");
-  const bool pipelined = sel && strcmp(sel, "pipelined") == 0;
-  const bool synced = !(sel && (strcmp(sel, "classic") == 0 || pipelined));
-  const size_t lds_sync = sync_lds_bytes<T>(h->map_bytes);
-  if (synced && mode == kSynth && !io.log && io.auto_reset && h->use_index &&
-      lds_sync + sizeof(Consts<T>) + 256 <= kLdsSplitMax) {
-    const int mach = a.c.mach_simpl ? 1 : 0;
-    const void* kern = mach ? reinterpret_cast<const void*>(&k_env_steps_sync<T, 1>)
-                            : reinterpret_cast<const void*>(&k_env_steps_sync<T, 0>);
-    if (h->lds_attr_sync[mach] != (int)lds_sync) {
-      HIP_TRY(h, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sync));
-      h->lds_attr_sync[mach] = (int)lds_sync;
-    }
-    const int gs = kSyncGroups;
-    const int blocks2 = (h->n_env + gs * kWave - 1) / (gs * kWave);
-    if (mach) hipLaunchKernelGGL((k_env_steps_sync<T, 1>), dim3(blocks2), dim3(256 * gs), lds_sync, stream, a);
-    else hipLaunchKernelGGL((k_env_steps_sync<T, 0>), dim3(blocks2), dim3(256 * gs), lds_sync, stream, a);
-    HIP_TRY(h, hipGetLastError());
-    return SIT_OK;
-  }
-  const size_t lds_split = split_lds_bytes<T>(h->map_bytes);
-  if (pipelined && mode == kSynth && !io.log && io.auto_reset && h->use_index &&
-      lds_split + sizeof(Consts<T>) + 256 <= kLdsSplitMax) {
-    const int mach = a.c.mach_simpl ? 1 : 0;
-    const void* kern = mach ? reinterpret_cast<const void*>(&k_env_steps_split<T, 1>)
-                            : reinterpret_cast<const void*>(&k_env_steps_split<T, 0>);
-    if (h->lds_attr_split[mach] != (int)lds_split) {
-      HIP_TRY(h, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_split));
-      h->lds_attr_split[mach] = (int)lds_split;
-    }
-    const int blocks2 = (h->n_env + 2 * kWave - 1) / (2 * kWave);
-    if (mach) hipLaunchKernelGGL((k_env_steps_split<T, 1>), dim3(blocks2), dim3(512), lds_split, stream, a);
-    else hipLaunchKernelGGL((k_env_steps_split<T, 0>), dim3(blocks2), dim3(512), lds_split, stream, a);
-    HIP_TRY(h, hipGetLastError());
-    return SIT_OK;
-  }
   int rc;
   if (mode == kSynth) rc = pick(std::integral_constant<int, kSynth>{});
   else if (mode == kPolicy) rc = pick(std::integral_constant<int, kPolicy>{});
   else rc = pick(std::integral_constant<int, kExplicit>{});
   if (rc) return rc;
   HIP_TRY(h, hipGetLastError());
+  set_kernel_name<T>(h, false, mode, lds_map, io.log != nullptr, mach);
   return SIT_OK;
 }
 

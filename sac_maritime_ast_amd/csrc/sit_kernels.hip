@@ -6,7 +6,7 @@
 
 namespace {
 
-#ifdef SIT_SPLIT_F32
+#ifdef SIT_F32_TU
 }  // namespace
 int sit_launch_steps_f32(sit_handle* h, const void* io, void* stream);   // sit_steps_f32.hip
 int sit_launch_probe_f32(sit_handle* h, int n, const void* pts_ne, void* dist, uint8_t* inside, uint8_t* hull,
@@ -41,7 +41,7 @@ int launch_selftest_f32tu(int op, int n, const double* a, const double* b, doubl
 // =======================================================================================
 extern "C" {
 
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SPLIT)
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
 #ifdef SIT_DIAG_PHASES
 int sit_diag_read_waves(unsigned long long* out, int n) {   // [n][4], diagnostic builds only
   if (hipDeviceSynchronize() != hipSuccess) return -1;
@@ -198,6 +198,7 @@ void sit_params_default(sit_params* p) {
 const char* sit_last_error(const sit_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
 int32_t sit_precision(const sit_handle* h) { return h ? h->precision : 0; }
 int32_t sit_n_env(const sit_handle* h) { return h ? h->n_env : 0; }
+const char* sit_step_kernel(const sit_handle* h) { return h ? h->last_kernel : ""; }
 int32_t sit_state_nfields(void) { return kNumFields; }
 
 int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t precision, sit_handle** out) {
@@ -221,6 +222,9 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
   h->n_env = n_env;
   h->cap = wpt_capacity;
   h->p = *p;
+  // diagnostic kernel selection (read once; the launch path reads no environment)
+  if (const char* sel = getenv("SIT_STEP_KERNEL")) h->kernel_classic = strcmp(sel, "classic") == 0;
+  if (const char* lm = getenv("SIT_LDS_MAP")) h->lds_map_sel = (lm[0] == '0') ? 0 : (lm[0] == '1') ? 1 : -1;
   hipError_t e = setup_device(&h->device);
   if (e != hipSuccess) { fail(nullptr, SIT_E_HIP, "hipGetDevice: %s", hipGetErrorString(e)); delete h; return SIT_E_HIP; }
   const size_t rs = real_size(h);

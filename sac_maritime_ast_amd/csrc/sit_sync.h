@@ -1,29 +1,49 @@
 // sit_sync.h — the step kernel with each ship's map predicates on a wave of their own, in the
-// same step (no speculation): synthetic-sampler rollouts with auto-reset (configs C3/C4).
+// same step (no speculation): rollouts with auto-reset whose actions come from the synthetic AST
+// sampler (configs C3/C4) or from the SAC policy between launches (config C5).
 //
-// Included from sit_impl.h (inside its anonymous namespace, after sit_split.h).
+// Included from sit_impl.h (inside its anonymous namespace, after k_env_steps).
 //
 // Forward Euler moves a ship with its pre-step velocities and heading (ship_model.py:632-643), so
 // the post-step position is known at the start of the step.  The D wave of each ship publishes it
-// (and the obstacle's IW of the step) before barrier A, then runs the sampler, guidance, control,
-// machinery and kinetics; meanwhile the ship's P wave evaluates the map predicates of that
-// position (boundary distance, hull in terrain, the IW test; MSRL_env_ex.py:490-542, 628-881).
-// Barrier B joins them: D decides the episode's end and runs the auto reset, P turns the distance
-// into the reward terms, and P0, one step behind, writes reward / done / status and the replay
-// transition.  Roles as in sit_split.h: 512-thread blocks of 2 env groups x {D0, D1, P0, P1},
-// mirrored in group 1 so each SIMD holds one D and one P wave.
+// (and the obstacle's IW of the step) before barrier A, then runs guidance, control, machinery and
+// kinetics; meanwhile the ship's P wave evaluates the map predicates of that position (boundary
+// distance, hull in terrain, the IW test; MSRL_env_ex.py:490-542, 628-881).  Barrier B joins them:
+// D decides the episode's end and runs the auto reset, P turns the distance into the reward terms,
+// and P0, one step behind, writes reward / done / status and the replay transition.
+//
+// Roles: a 256-thread block is one env group of kSyncLanes envs x {D0, D1, P0, P1}; odd blocks take
+// the roles in mirrored order (P0 P1 D0 D1), which aims each SIMD at one D and one P wave.
+//
+// Policy mode (MODE == kPolicy, the sampler of samplers.PolicySampler): at a sampling event D1
+// consumes the env's action slot if the policy has filled it; otherwise the env takes no further
+// step in this launch (all four waves skip it: D1 publishes the decision before barrier A), D1
+// queues the request (env id, the event's standard-normal draw) and P0, which holds the env's
+// observation, writes the request's observation row and the ST_NO_STEP rows.
 #pragma once
 
-#ifndef SIT_SYNC_GROUPS
-#define SIT_SYNC_GROUPS 1   // env groups per block: 1 = 256-thread blocks, two per CU, role order by block parity
-                            // (2 groups in 512-thread blocks measured 8 % slower: barriers couple the groups)
+#ifndef SIT_SYNC_LANES
+#define SIT_SYNC_LANES 64   // envs per group (active lanes of each of the group's four waves)
 #endif
-#define SIT_SYNC_GROUPS_LDS SIT_SYNC_GROUPS
+#ifndef SIT_SYNC_CREF
+#define SIT_SYNC_CREF 1     // D waves read the constants from their LDS copy (no VGPR spills; +2.5 %)
+#endif
+constexpr int kSyncLanes = SIT_SYNC_LANES;
+static_assert(kSyncLanes >= 1 && kSyncLanes <= kWave, "SIT_SYNC_LANES must be in [1, 64]");
+
+// D-wave flags of a step (kSf*), per ship
+constexpr uint32_t kSfArrive = 1u << 0, kSfHorizon = 1u << 1, kSfNav = 1u << 2, kSfMech = 1u << 3,
+                   kSfEct = 1u << 4, kSfBlk = 1u << 5, kSfStopPre = 1u << 8, kSfDoneNt = 1u << 9,
+                   kSfSac = 1u << 10, kSfOverflow = 1u << 11;
+// the step's policy-mode decision (SyncSlot::q): the env steps / it stopped earlier in this launch;
+// q >= 0: it stops at this step and its request went to slot q of the queue
+constexpr int32_t kQLive = -1, kQStalled = -2;
 
 template <typename T>
-struct SyncSlot {             // one step of the 64 envs of a group (ring of 2)
+struct SyncSlot {             // one step of the envs of a group (ring of 2)
   T pn[2][kWave], pe[2][kWave];   // post-step position per ship (D, before A)
   T iwn[kWave], iwe[kWave];       // the obstacle's IW of the step (D1, before A)
+  int32_t q[kWave];               // policy mode: kQLive / kQStalled / request slot (D1, before A)
   T t[6][kWave];              // test ship: n, e, psi, rpm, |e_ct|, P_me (D0, before B)
   T o[5][kWave];              // obstacle: n, e, psi, |e_ct|, SAC action (D1, before B)
   uint32_t f[2][kWave];       // kSf* flags per ship (D, before B)
@@ -39,15 +59,15 @@ struct SyncShared {
 
 template <typename T>
 __host__ __device__ constexpr size_t sync_lds_bytes(size_t map_bytes) {
-  return ((map_bytes + 255) & ~size_t(255)) + SIT_SYNC_GROUPS_LDS * ((sizeof(SyncShared<T>) + 255) & ~size_t(255));
+  return ((map_bytes + 255) & ~size_t(255)) + ((sizeof(SyncShared<T>) + 255) & ~size_t(255));
 }
 
 // ------------------------------------------------------------------------------------------
 // D waves
 // ------------------------------------------------------------------------------------------
-template <typename T, int TYPE, int MACH>
+template <typename T, int MODE, int TYPE, int MACH>
 __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, SyncShared<T>& X, int env, bool act) {
-#if SIT_SPLIT_CREF
+#if SIT_SYNC_CREF
   const Consts<T>& c = cs;
 #else
   const Consts<T> c = cs;
@@ -64,6 +84,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   int ep_step = 0;
   uint32_t event = 0, episodes = 0;
   double ab_len = 0.0, ab_alpha = 0.0, samp_limit = 0.0;
+  // policy mode: the env's action slot (D1), and whether the env stopped for the policy
+  bool ready = false, stalled = false;
+  T pa = T(0);
   if (act) {
     ep_step = a.st.ep_step[env];
     load_ship(a.st, sid, s);
@@ -84,6 +107,10 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       ab_len = a.sc.ab_len[env];
       ab_alpha = a.sc.ab_alpha[env];
       samp_limit = ieee_mul(ab_len, cs.x.theta);   // MSRL_env_ex.py:569
+      if (MODE == kPolicy) {
+        ready = a.io.policy_ready[env] != 0;
+        pa = a.io.policy_action[env];
+      }
     }
   }
   T p0[6] = {};
@@ -111,26 +138,45 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     T n1 = s.n, e1 = s.e;
     bool sac = false;
     double ang = 0.0, act_n = 0.0;
-    if (act) {
+    if (act && !stalled) {
       xsincos(s.psi, &sp, &cp);
       if (TYPE == 0 || !s.stop) euler_position(c, s, sp, cp, n1, e1);
       if (TYPE == 1) {
-        // synthetic AST sampler (uniform_policy.py:20-22 scaled by pi/6): the IW of
-        // this step is published with the position, for P1's IW test
+        // a sampling event: the episode's first step, or the sampling distance reaching AB_len while
+        // the obstacle ship runs (test_beds/main_ast.py:337-349 with the SURVEY 8(d) converter)
         sac = ep_step == 0 || ((double)samp >= ab_len && !s.stop);
-        if (sac) {
-          const double u01 = sampler_uniform(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
-          act_n = u01 * 2.0 - 1.0;
-          ang = act_n * (M_PI / 6.0);
+        int32_t q = kQLive;
+        if (MODE == kPolicy && sac && !ready) {
+          // no action yet: the env waits for the policy; queue the request with this event's
+          // standard-normal draw (the reparameterised sample, normal.py:96-101)
+          stalled = true;
+          sac = false;
+          q = atomicAdd(a.io.request_count, 1);
+          if (q < a.io.request_capacity) {
+            a.io.request_env[q] = env;
+            a.io.request_noise[q] = (T)sampler_normal(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
+          }
+        } else if (sac) {
+          if (MODE == kPolicy) {          // the policy's squashed action in [-1, 1]
+            act_n = (double)pa;
+            ready = false;
+          } else {                        // mode-0 action U[-1, 1] (uniform_policy.py:20-22)
+            act_n = sampler_uniform(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event) * 2.0 - 1.0;
+          }
+          ang = act_n * (M_PI / 6.0);    // the route angle, scaled by the action bound pi / 6
           iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
           ++event;
         }
+        if (MODE == kPolicy) xd.q[lane] = q;
         xd.iwn[lane] = iwn; xd.iwe[lane] = iwe;
       }
       xd.pn[TYPE][lane] = n1; xd.pe[TYPE][lane] = e1;
+    } else if (MODE == kPolicy && TYPE == 1 && act) {
+      xd.q[lane] = kQStalled;
     }
-    __syncthreads();   // A: positions (and the IW) published
-    if (act) {
+    __syncthreads();   // A: positions (and the IW, and in policy mode the step's decision) published
+    if (MODE == kPolicy && TYPE == 0 && act && !stalled) stalled = xd.q[lane] != kQLive;
+    if (act && !stalled) {
       T o_rpm, o_ect, o_pme = T(0);
       bool ect_over = false;
       uint32_t fl = s.stop ? kSfStopPre : 0u;
@@ -211,7 +257,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     }
     __syncthreads();   // B: both ships' step and their map predicates
     // the episode's end (every predicate, the collision) and the auto reset (main_ast.py:314-333)
-    if (act) {
+    if (act && !stalled) {
       const T tn = xd.t[0][lane], te = xd.t[1][lane], on = xd.o[0][lane], oe = xd.o[1][lane];
       const bool coll = closer_than(tn, te, on, oe, c.coll_d2);
       const bool env_done = ((xd.f[0][lane] | xd.f[1][lane]) & kSfDoneNt) || ((xd.pb[0][lane] | xd.pb[1][lane]) & 7u) ||
@@ -245,6 +291,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       a.st.ep_step[env] = ep_step;
       a.st.event[env] = event;
       a.st.episodes[env] = episodes;
+      if (MODE == kPolicy) a.io.policy_ready[env] = ready ? 1 : 0;
     }
   }
 }
@@ -252,7 +299,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
 // ------------------------------------------------------------------------------------------
 // P waves
 // ------------------------------------------------------------------------------------------
-template <typename T, int TYPE>
+template <typename T, int MODE, int TYPE>
 __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, const Map<T>& map_in,
                                       SyncShared<T>& X, int env, bool act) {
   const Consts<T> c = cs;
@@ -269,6 +316,8 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   uint32_t bits_t = 0;
   T dobst = T(0);
   bool terrain = false, iw_term = false;
+  bool stalled = false;             // policy mode: the env stopped for the policy in this launch
+  uint32_t n_stepped = 0;           // policy mode (P0): env-steps executed
   uint32_t uf = __builtin_amdgcn_readfirstlane((a.io.reward ? 2u : 0u) | (a.io.done ? 4u : 0u) |
                                                (a.io.status ? 8u : 0u) | (a.io.transitions ? kUfTrans : 0u) |
                                                (a.io.done_count ? kUfDoneCnt : 0u) |
@@ -278,7 +327,21 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   auto outputs = [&](int j) {
     const SyncSlot<T>& xd = X.d[j & 1];
     bool env_done = false;
-    if (act) {
+    bool live = act;
+    if (MODE == kPolicy && act) {
+      const int32_t q = xd.q[lane];
+      live = q == kQLive;
+      if (!live) {                     // no step in this row: the env waits for its action
+        const size_t row = (size_t)j * n_env + env;
+        if (uf & 8) a.io.status[row] = SIT_ST_NO_STEP;
+        if (uf & 4) a.io.done[row] = 0;
+        if (q >= 0 && q < a.io.request_capacity)
+          for (int k = 0; k < SIT_OBS_DIM; ++k) a.io.request_obs[(size_t)q * SIT_OBS_DIM + k] = lo[k];
+      } else {
+        ++n_stepped;
+      }
+    }
+    if (live) {
       const T tn = xd.t[0][lane], te = xd.t[1][lane], on = xd.o[0][lane], oe = xd.o[1][lane];
       const bool coll = closer_than(tn, te, on, oe, c.coll_d2);
       const uint32_t bo = xd.bo[lane];
@@ -333,8 +396,9 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     SyncSlot<T>& xd = X.d[it & 1];
     __syncthreads();   // A: this step's positions
     if (TYPE == 0 && it >= 1) outputs(it - 1);
+    if (MODE == kPolicy && act && !stalled) stalled = xd.q[lane] != kQLive;
     // the map predicates of the post-step position (MSRL_env_ex.py:490-542, 628-881)
-    if (act) {
+    if (act && !stalled) {
       const T sn = xd.pn[TYPE][lane], se = xd.pe[TYPE][lane];
       DistPf<T> pf;
       pf_cell(c, map, sn, se, pf);
@@ -354,7 +418,7 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       }
     }
     __syncthreads();   // B: the D waves' step results
-    if (act) {
+    if (act && !stalled) {
       const uint32_t fl = xd.f[TYPE][lane];
       int stop = (fl & kSfStopPre) ? 1 : 0;
       bool done = false;
@@ -409,36 +473,30 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     if (n >= 1) outputs(n - 1);
     if (act)
       for (int j = 0; j < SIT_OBS_DIM; ++j) a.st.last_obs[(size_t)j * n_env + env] = lo[j];
+    if (MODE == kPolicy && a.io.env_steps) {   // env-steps executed: one atomic per wave
+      unsigned long long v = act ? n_stepped : 0;
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0 && v) atomicAdd(a.io.env_steps, v);
+    }
   }
 }
 
-constexpr int kSyncGroups = SIT_SYNC_GROUPS;
-
-template <typename T, int MACH>
-__global__ __launch_bounds__(128 * kSyncGroups * 2) void k_env_steps_sync(const KArgs<T> a) {
+template <typename T, int MODE, int MACH>
+__global__ __launch_bounds__(256) void k_env_steps_sync(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Consts<T> cs;
   for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
     reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
   const Map<T> map = stage_map(a, smem);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int group = w >> 2;
-  const int flip = kSyncGroups == 1 ? (int)(blockIdx.x & 1) : group;
-  const int role = flip == 0 ? (w & 3) : ((w & 3) ^ 2);
+  const int role = (blockIdx.x & 1) == 0 ? w : (w ^ 2);
   const int lane = threadIdx.x & (kWave - 1);
-  const int env = (blockIdx.x * kSyncGroups + group) * kWave + lane;
-  const bool act = env < a.n_env;
-  SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(
-      smem + (((size_t)a.map_bytes + 255) & ~size_t(255)) +
-      (size_t)group * ((sizeof(SyncShared<T>) + 255) & ~size_t(255)));
+  const int env = blockIdx.x * kSyncLanes + lane;
+  const bool act = lane < kSyncLanes && env < a.n_env;
+  SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(smem + (((size_t)a.map_bytes + 255) & ~size_t(255)));
   __syncthreads();   // constants copied, map staged
-#ifndef SIT_SYNC_PRIO
-#define SIT_SYNC_PRIO 0
-#endif
-  if (SIT_SYNC_PRIO == 1 && role < 2) __builtin_amdgcn_s_setprio(1);        // D waves first
-  if (SIT_SYNC_PRIO == 2 && role == 1) __builtin_amdgcn_s_setprio(1);       // the obstacle's D wave first
-  if (role == 0) sync_d<T, 0, MACH>(a, cs, X, env, act);
-  else if (role == 1) sync_d<T, 1, MACH>(a, cs, X, env, act);
-  else if (role == 2) sync_p<T, 0>(a, cs, map, X, env, act);
-  else sync_p<T, 1>(a, cs, map, X, env, act);
+  if (role == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, env, act);
+  else if (role == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, env, act);
+  else if (role == 2) sync_p<T, MODE, 0>(a, cs, map, X, env, act);
+  else sync_p<T, MODE, 1>(a, cs, map, X, env, act);
 }

@@ -174,11 +174,12 @@ class VecMultiShipRLEnv:
                 actions: dict | None = None, out: dict | None = None, want=("next_state", "reward", "done",
                                                                               "status", "action", "done_count"),
                 transition_capacity: int = 0, mask_horizon: int = 600, policy_io: dict | None = None,
-                log: bool = False):
+                log: bool = False, reset_transitions: bool = True):
         """K fused steps (one kernel launch).  actions=None: synthetic AST sampler on device.
         Returns a dict of [K, n_env, ...] tensors (reused from `out` when given).  With
         transition_capacity > 0 the sampling-event replay transitions are appended to
-        out["transitions"] ([capacity, 24]) and counted in out["transition_count"] ([1]).
+        out["transitions"] ([capacity, 24]) and counted in out["transition_count"] ([1]); the count
+        is zeroed first unless reset_transitions=False (several launches appending to one buffer).
         policy_io: the policy-mode buffers (see samplers.PolicySampler): actions of sampling events
         come from a policy run between launches; waiting envs' rows carry status ST_NO_STEP."""
         n, K = self.n_env, int(n_steps)
@@ -213,7 +214,8 @@ class VecMultiShipRLEnv:
                                                  dtype=self.dtype, device=self.device)
             if out.get("transition_count") is None:
                 out["transition_count"] = torch.zeros(1, dtype=torch.int32, device=self.device)
-            out["transition_count"].zero_()
+            if reset_transitions:
+                out["transition_count"].zero_()
             ra.transitions = out["transitions"].data_ptr()
             ra.transition_count = out["transition_count"].data_ptr()
             ra.transition_capacity = int(transition_capacity)

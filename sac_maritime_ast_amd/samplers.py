@@ -147,6 +147,9 @@ class PolicySampler:
         if self._w is not None:
             self._w = self._w.to(dev)
             self._w_version = self._weights_version()
+        # the counter slot the next launch appends to was cleared by the previous launch's actor (the
+        # fused actor clears the other slot); an act() outside launch() leaves it holding a count
+        self._slot_clean = True
 
     @property
     def fused(self) -> bool:
@@ -166,17 +169,26 @@ class PolicySampler:
         """Env-steps executed so far (device int64[1])."""
         return self.io["env_steps"]
 
-    def launch(self, want=("next_state", "reward", "done", "status", "action")):
+    def launch(self, want=("next_state", "reward", "done", "status", "action"), events=None,
+               first: bool = True):
         """One fused launch of `chunk` steps followed by the actor on the queued requests.
-        Returns the launch's [K, n_env, ...] outputs (rows of waiting envs: status ST_NO_STEP)."""
+        Returns the launch's [K, n_env, ...] outputs (rows of waiting envs: status ST_NO_STEP).
+        events: optional (start, end) torch.cuda.Event pair recorded around the env kernel.
+        first: the launch starts a new batch of replay transitions (their count is zeroed); later
+        launches of a batch append to it, so a HIP graph of several launches keeps all of them."""
         p = self._slot
         self.io["request_count"] = self._counts[p:p + 1]
-        if self._w is None:       # the fused actor clears the slot of the next launch itself
+        if self._w is None or not self._slot_clean:
             self.io["request_count"].zero_()
+        if events is not None:
+            events[0].record(torch.cuda.current_stream(self.env.device))
         self.env.rollout(self.chunk, seed=self.seed, env_id_offset=self.env_id_offset, out=self.out,
                          want=want, transition_capacity=self.transition_capacity,
-                         mask_horizon=self.mask_horizon, policy_io=self.io)
+                         mask_horizon=self.mask_horizon, policy_io=self.io, reset_transitions=first)
+        if events is not None:
+            events[1].record(torch.cuda.current_stream(self.env.device))
         self.act()
+        self._slot_clean = True
         self._slot ^= 1
         return self.out
 
@@ -192,8 +204,8 @@ class PolicySampler:
         torch.cuda.synchronize(self.env.device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            for _ in range(n_launch):
-                self.launch(want)
+            for i in range(n_launch):
+                self.launch(want, first=(i == 0))
         return self
 
     def replay(self):
@@ -208,6 +220,7 @@ class PolicySampler:
         (sit_policy_apply), or for policies without a `.net` (mu, log_sigma) trunk forward() and a
         device-side scatter."""
         io, env = self.io, self.env
+        self._slot_clean = False             # launch() marks it clean again after its own act()
         if self._w is not None:
             if not torch.cuda.is_current_stream_capturing() and self._weights_version() != self._w_version:
                 self.refresh_weights()
@@ -249,13 +262,14 @@ class OverlappedPolicySampler:
         dev = device or samplers[0].env.device
         self.streams = [torch.cuda.Stream(device=dev) for _ in samplers]
 
-    def launch(self, want=("next_state", "reward", "done", "status", "action")):
+    def launch(self, want=("next_state", "reward", "done", "status", "action"), events=None, first: bool = True):
+        """One launch of every group on its stream; events: optional per-group (start, end) pairs."""
         cur = torch.cuda.current_stream(self.streams[0].device)
         outs = []
-        for sm, st in zip(self.samplers, self.streams):
+        for g, (sm, st) in enumerate(zip(self.samplers, self.streams)):
             st.wait_stream(cur)
             with torch.cuda.stream(st):
-                outs.append(sm.launch(want))
+                outs.append(sm.launch(want, events=None if events is None else events[g], first=first))
         for st in self.streams:
             cur.wait_stream(st)
         return outs
@@ -273,8 +287,8 @@ class OverlappedPolicySampler:
         torch.cuda.synchronize(self.streams[0].device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            for _ in range(n_launch):
-                self.launch(want)
+            for i in range(n_launch):
+                self.launch(want, first=(i == 0))
         return self
 
     def replay(self):

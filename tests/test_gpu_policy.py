@@ -250,3 +250,226 @@ def test_fused_actor_policy_mode_sanity():
         live = (st & _lib.ST_NO_STEP) == 0
         assert torch.isfinite(out["next_state"][live]).all()
         assert int(s.served.item()) > n_env
+
+
+# ------------------------------------------------------------------------------------------
+# float32 policy mode: the instantiation config C5 times (k_env_steps_sync<float, kPolicy>)
+# ------------------------------------------------------------------------------------------
+def _f32_rounded(st):
+    return {k: (v.astype(np.float32).astype(np.float64) if v.dtype == np.float64 else v) for k, v in st.items()}
+
+
+def _np_state(env):
+    return {k: v.cpu().numpy() for k, v in env.get_state().items()}
+
+
+def _policy_io(n_env, cap, dtype):
+    io = {"policy_action": torch.zeros(n_env + 1, dtype=dtype, device=DEV),
+          "policy_ready": torch.zeros(n_env + 1, dtype=torch.int32, device=DEV),
+          "request_env": torch.full((cap,), -1, dtype=torch.int32, device=DEV),
+          "request_noise": torch.zeros(cap, dtype=dtype, device=DEV),
+          "request_obs": torch.zeros((cap, _lib.SIT_OBS_DIM), dtype=dtype, device=DEV),
+          "request_count": torch.zeros(1, dtype=torch.int32, device=DEV),
+          "env_steps": torch.zeros(1, dtype=torch.int64, device=DEV)}
+    return io
+
+
+def _rel(a, b, scale):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return np.abs(a - b) / np.maximum(np.abs(b), scale)
+
+
+SCALE_F = dict(north=1e4, east=1e4, yaw=np.pi, surge=10.0, sway=10.0, yaw_rate=0.1, shaft_speed=100.0,
+               ship_speed_i=1e3, shaft_speed_i=1e5, heading_i=10.0, heading_prev=np.pi, e_ct_int=1e2,
+               last_rpm=1e3, last_e_ct=1e3, last_power_me=1e3, sampling_dist=1e4, eps_dist=1e4,
+               prev_pre_north=1e4, prev_pre_east=1e4, iw_north=1e4, iw_east=1e4)
+
+
+def test_f32_policy_mode_step_vs_oracle():
+    """One policy-mode step of the float32 kernel C5 runs, from float32-rounded states of 4096 envs at
+    six episode depths, against the oracle's synchronous loop (OracleEnvs.policy_rollout, the loop of
+    test_beds/main_ast.py:337-396) on the same state and actions.  At each depth a quarter of the envs
+    are put at a sampling event (episode start or sampling distance >= AB_len); two thirds of those
+    hold a ready action (policy_ready, an action in [-1, 1]) and step, the others wait for the policy.
+    Stepping envs: next_state, reward, IW and post-state within 1e-5 relative (per-field floors);
+    done, status, waypoint index, route length, stop flags, counters and replay transitions' discrete
+    fields identical.  Waiting envs: ST_NO_STEP rows with done 0, state untouched, and their request
+    (env id, observation, the event's normal draw) queued."""
+    n_env = 4096
+    sc = make_scenario(n_env, cap=32, seed=31)
+    env64 = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+    env64.reset()
+    env64.init_step()
+    env32 = VecMultiShipRLEnv(scenario=sc, precision=32, device=DEV)
+    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+    worst, n_live_ev, n_wait = {}, 0, 0
+
+    def upd(k, v):
+        worst[k] = max(worst.get(k, 0.0), float(v))
+    for depth in range(6):
+        env64.rollout(300, seed=50 + depth)
+        st = _f32_rounded(_np_state(env64))
+        rng = np.random.default_rng(depth)
+        # put a quarter of the envs at a sampling event (a third of those at an episode start)
+        ev = rng.random(n_env) < 0.25
+        start = ev & (rng.random(n_env) < 0.33)
+        st["ep_step"] = np.where(start, 0, st["ep_step"])
+        run = ev & ~start & (st["stop"][1] == 0)
+        st["sampling_dist"] = np.where(run, np.float32(o.ab_len * 1.0001), st["sampling_dist"]).astype(np.float64)
+        st["sampling_dist"] = st["sampling_dist"].astype(np.float32).astype(np.float64)
+        need = (st["ep_step"] == 0) | ((st["sampling_dist"] >= o.ab_len) & (st["stop"][1] == 0))
+        ready = need & (rng.random(n_env) < 0.67)
+        wait = need & ~ready
+        act = rng.uniform(-1, 1, n_env).astype(np.float32)
+        o.set_state(st)
+        env32.set_state(st)
+        io = _policy_io(n_env, n_env, torch.float32)
+        io["policy_action"][:n_env] = torch.from_numpy(act).to(DEV)
+        io["policy_ready"][:n_env] = torch.from_numpy(ready.astype(np.int32)).to(DEV)
+        seed = 700 + depth
+        out = env32.rollout(1, seed=seed, policy_io=io, transition_capacity=2 * n_env, mask_horizon=600)
+        assert "kPolicy" in env32.lib.sit_step_kernel(env32.handle).decode()
+        post = _np_state(env32)
+        live = ~wait
+
+        def policy_fn(state, noise):
+            return act[np.nonzero(need)[0]].astype(np.float64)
+        r = o.policy_rollout(1, seed, policy_fn, mask_horizon=600)
+        ref = o.get_state()
+        # stepping envs
+        ns, rew = out["next_state"][0].cpu().numpy(), out["reward"][0].cpu().numpy()
+        upd("next_state", _rel(ns[live], r["next_state"][0][live], OBS_SCALE).max())
+        upd("reward", _rel(rew[live], r["reward"][0][live], 1.0).max())
+        done = out["done"][0].cpu().numpy().astype(bool)
+        stat = out["status"][0].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        assert np.array_equal(done[live], r["done"][0][live]), f"depth {depth}: done"
+        assert np.array_equal(stat[live], r["status"][0][live].astype(np.int64)), f"depth {depth}: status"
+        a = out["action"][0].cpu().numpy().astype(np.float64)
+        sac = r["action"][0, :, 3] > 0.5
+        assert np.array_equal(a[live, 3] > 0.5, sac[live]), f"depth {depth}: sampling events"
+        ev_live = live & sac
+        n_live_ev += int(ev_live.sum())
+        upd("iw", _rel(a[ev_live, :2], r["action"][0, ev_live, :2], 1e4).max() if ev_live.any() else 0.0)
+        for k in so.SHIP_REAL:
+            upd(k, _rel(post[k][:, live], ref[k][:, live], SCALE_F[k]).max())
+        for k in so.ENV_REAL:
+            upd(k, _rel(post[k][live], ref[k][live], SCALE_F[k]).max())
+        for k in so.SHIP_INT:
+            assert np.array_equal(post[k][:, live], ref[k][:, live].astype(post[k].dtype)), f"depth {depth}: {k}"
+        for k in so.ENV_INT:
+            assert np.array_equal(post[k][live].astype(np.int64), ref[k][live].astype(np.int64)), f"depth {depth}: {k}"
+        # the consumed action slots are cleared, the others keep their flag
+        rd = io["policy_ready"][:n_env].cpu().numpy()
+        assert np.array_equal(rd, (ready & ~need).astype(np.int32)), f"depth {depth}: policy_ready"
+        # replay transitions of the stepping envs' events (per env id; the kernel appends with atomics)
+        cnt = int(out["transition_count"].item())
+        got = out["transitions"][:cnt].cpu().numpy().astype(np.float64)
+        want = r["transitions"]
+        want = want[live[want[:, 23].astype(np.int64)]]
+        assert cnt == len(want), f"depth {depth}: transitions {cnt} vs {len(want)}"
+        if cnt:
+            got, want = got[np.argsort(got[:, 23])], want[np.argsort(want[:, 23])]
+            assert np.array_equal(got[:, 23], want[:, 23]) and np.array_equal(got[:, 22], want[:, 22])
+            assert np.abs(got[:, 10] - want[:, 10]).max() <= 1e-7         # the policy's action
+            cols = np.r_[0:10, 12:22]
+            upd("transitions", _rel(got[:, cols], want[:, cols], np.r_[OBS_SCALE, OBS_SCALE]).max())
+        # waiting envs: no step, state untouched, request queued
+        n_wait += int(wait.sum())
+        assert np.all(stat[wait] == _lib.ST_NO_STEP) and not done[wait].any(), f"depth {depth}: waiting rows"
+        for k in so.SHIP_REAL + so.SHIP_INT:
+            assert np.array_equal(post[k][:, wait], st[k][:, wait].astype(post[k].dtype)), f"depth {depth}: {k} moved"
+        for k in so.ENV_REAL + so.ENV_INT:
+            assert np.array_equal(post[k][wait], st[k][wait].astype(post[k].dtype)), f"depth {depth}: {k} moved"
+        q = int(io["request_count"].item())
+        assert q == int(wait.sum()), f"depth {depth}: {q} requests for {int(wait.sum())} waiting envs"
+        renv = io["request_env"][:q].cpu().numpy()
+        assert np.array_equal(np.sort(renv), np.nonzero(wait)[0]), f"depth {depth}: request env ids"
+        robs = io["request_obs"][:q].cpu().numpy().astype(np.float64)
+        assert np.array_equal(robs, st["last_obs"].T[renv]), f"depth {depth}: request observations"
+        noise = so.sampler_normal(seed, renv.astype(np.uint64), st["event"][renv])
+        assert np.abs(io["request_noise"][:q].cpu().numpy() - noise).max() <= 1e-6 * max(1.0, np.abs(noise).max())
+        assert int(io["env_steps"].item()) == int(live.sum())
+    print("f32 policy-mode step worst:", {k: f"{v:.2e}" for k, v in worst.items()},
+          f"events stepped {n_live_ev}, envs waiting {n_wait}")
+    bad = {k: f"{v:.2e}" for k, v in worst.items() if v > 1e-5}
+    assert not bad, bad
+    assert n_live_ev > 1000 and n_wait > 500
+
+
+def _executed_rows(outs_list, n_env):
+    """Per env, the executed (status without ST_NO_STEP) rows of a list of launch outputs."""
+    seq = [[] for _ in range(n_env)]
+    for o in outs_list:
+        st = o["status"].astype(np.int64) & 0xFFFFFFFF
+        live = (st & _lib.ST_NO_STEP) == 0
+        for k in range(st.shape[0]):
+            for e in np.nonzero(live[k])[0]:
+                seq[e].append((o["next_state"][k, e], o["reward"][k, e], int(st[k, e])))
+    return seq
+
+
+def test_f32_c5_size_fused_actor_graph_replay():
+    """Config C5 at its configured size: 65 536 ships (2 groups x 16 384 envs) on two streams, the fused
+    256x256 actor, 16 launches per HIP graph, as bench.py --mode policy runs it.  Properties: the
+    executed rows account for the device env-step counter, ST_NO_STEP rows carry done 0, outputs are
+    finite, the policy served every
+    group more than once per env; and batching independence: the first 512 envs of group 0, run as a
+    512-env handle with the same global ids and policy, execute bit-identical rows."""
+    n, G, chunk, per_graph = 16384, 2, 32, 16
+    pol = make_policy256(DEV)
+    samplers = []
+    for g in range(G):
+        env = VecMultiShipRLEnv(scenario=make_scenario(n, cap=48, seed=25450, env_offset=g * n), precision=32,
+                                device=DEV)
+        env.reset()
+        env.init_step()
+        samplers.append(PolicySampler(env, pol, chunk=chunk, seed=SEED, env_id_offset=g * n,
+                                      request_capacity=n // 4, transition_capacity=per_graph * chunk * n // 64))
+    assert all(s.fused for s in samplers)
+    ov = OverlappedPolicySampler(samplers).capture(per_graph)
+    assert "k_env_steps_sync<float,kPolicy" in samplers[0].env.lib.sit_step_kernel(samplers[0].env.handle).decode()
+    before = [int(s.env_steps.item()) for s in samplers]
+    rows_g0 = []
+    for rep in range(3):
+        outs = ov.replay()
+        torch.cuda.synchronize()
+        for s, out in zip(samplers, outs):
+            st = out["status"].to(torch.int64) & 0xFFFFFFFF
+            live = (st & _lib.ST_NO_STEP) == 0
+            assert torch.isfinite(out["next_state"][live]).all() and torch.isfinite(out["reward"][live]).all()
+            assert not out["done"][~live].any()
+            # the graph's launches append their replay transitions to one buffer: at least the last
+            # launch's sampling events, none dropped
+            ev = (out["action"][..., 3] > 0.5) & live
+            cnt = int(out["transition_count"].item())
+            assert int(ev.sum().item()) <= cnt <= s.transition_capacity, (int(ev.sum().item()), cnt)
+    stepped = [int(s.env_steps.item()) - b for s, b in zip(samplers, before)]
+    for s in stepped:
+        assert s > 0.8 * 3 * per_graph * chunk * n, stepped
+    for s in samplers:
+        assert int(s.served.item()) > n
+    # batching independence (eager launches; the graph's launches are the same kernels)
+    m = 512
+    envs = []
+    for nn in (n, m):
+        env = VecMultiShipRLEnv(scenario=make_scenario(nn, cap=48, seed=25450, env_offset=0), precision=32,
+                                device=DEV)
+        env.reset()
+        env.init_step()
+        sm = PolicySampler(env, pol, chunk=chunk, seed=SEED, env_id_offset=0, request_capacity=nn // 4)
+        outs = []
+        for _ in range(12):
+            o = sm.launch()
+            torch.cuda.synchronize()
+            outs.append({k: o[k][:, :m].cpu().numpy().copy() for k in ("next_state", "reward", "status")})
+        envs.append(_executed_rows(outs, m))
+    big, small = envs
+    compared = 0
+    for e in range(m):
+        k = min(len(big[e]), len(small[e]))
+        assert k >= 200, f"env {e}: {k} rows"
+        for i in range(k):
+            assert np.array_equal(big[e][i][0], small[e][i][0]) and big[e][i][1] == small[e][i][1] \
+                and big[e][i][2] == small[e][i][2], f"env {e} row {i}"
+        compared += k
+    assert compared > 100000

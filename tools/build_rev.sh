@@ -9,7 +9,7 @@ mkdir -p "$d/include" "$d/csrc" build_diag
 git show "$rev:include/sit.h" > "$d/include/sit.h"
 git show "$rev:sac_maritime_ast_amd/csrc/sit_device.h" > "$d/csrc/sit_device.h"
 git show "$rev:sac_maritime_ast_amd/csrc/sit_kernels.hip" > "$d/csrc/sit_kernels.hip"
-# single-TU build (no -DSIT_SPLIT_F32): pass "-Xarch_device -ffast-math" to match the float32 TU
+# single-TU build (no -DSIT_F32_TU): pass "-Xarch_device -ffast-math" to match the float32 TU
 for f in $(git ls-tree --name-only "$rev" sac_maritime_ast_amd/csrc/ | xargs -n1 basename | grep '\.h$'); do
   if git cat-file -e "$rev:sac_maritime_ast_amd/csrc/$f" 2>/dev/null; then
     git show "$rev:sac_maritime_ast_amd/csrc/$f" > "$d/csrc/$f"
