@@ -477,12 +477,14 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   }
   const T maxn = c.max_n;
   // episode-start values held in registers (auto-reset reloads nothing from memory): the
-  // construction pose, route length, first leg with its geometry, and initial observation
+  // construction pose, route length, first leg with its geometry, and initial observation.  Only
+  // with auto-reset: a launch without it (sit_step, explicit actions) skips these loads and the
+  // first leg's geometry in its prologue
   T p0[6] = {};
   T lo0[6] = {};
   int nw0 = 0;
   typename Route<T>::Leg leg0{};
-  if (act) {
+  if (act && __builtin_amdgcn_readfirstlane(a.io.auto_reset)) {
     for (int j = 0; j < 6; ++j) p0[j] = init_val(a.sc, type, SIT_INIT_NORTH + j, env, n_env);
     for (int j = 0; j < lo_n; ++j) lo0[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + lo_base + j];
     nw0 = a.sc.nw0[sid];

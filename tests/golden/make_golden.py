@@ -673,11 +673,60 @@ def gen_env_cases(ref, obstacle, env_mod, seed):
     return n
 
 
+# ---------------------------------------------------------------------------------
+# attribute paths the drop-in reads from the reference's objects (compat.ASSET_PATHS)
+# ---------------------------------------------------------------------------------
+def _jsonable(v):
+    if isinstance(v, (list, tuple, np.ndarray)):
+        return [_jsonable(x) for x in v]
+    if isinstance(v, (bool, np.bool_)):
+        return bool(v)
+    if isinstance(v, (int, np.integer)):
+        return int(v)
+    if isinstance(v, (float, np.floating)):
+        return float(v)
+    return v if isinstance(v, str) else repr(v)
+
+
+def gen_asset_paths(ref2, obstacle, env_mod):
+    """tests/golden/asset_paths.json: for the reference's own ShipAssets (test_beds/test_policy.py
+    objects, built as make_env does), the value at every attribute path compat.MultiShipRLEnv reads
+    (compat.ASSET_PATHS) -- after construction, and after reset / init_step / three steps with one IW
+    inserted -- plus the env's initial_state and AB segment.  Pins the drop-in's attribute names to
+    the reference's classes; the GPU tests build their stand-in objects from these paths."""
+    import json
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from sac_maritime_ast_amd import compat
+    out = {"paths": list(compat.ASSET_PATHS), "cases": {}}
+    for mode in ("PTI", "PTO"):
+        pose_test = (R_TEST[0][0], R_TEST[0][1], math.atan2(4000, 300), 0, 0, 0)
+        pose_obs = (R_OBS[0][0], R_OBS[0][1], math.atan2(-100, 6400), 0, 0, 0)
+        env = make_env(ref2, obstacle, env_mod, pose_test, pose_obs, mode=mode)
+        snap = lambda: {who: {p: _jsonable(compat._get(a, p, None)) for p in compat.ASSET_PATHS}  # noqa: E731
+                        for who, a in (("test", env.test), ("obs", env.obs))}
+        case = {"constructed": snap(), "initial_state": _jsonable(env.initial_state),
+                "AB_segment_length": float(env.AB_segment_length), "AB_alpha": float(env.AB_alpha)}
+        env.reset()
+        env.init_step()
+        iw = (env.obs.ship_model.north + 900.0, env.obs.ship_model.east + 50.0)
+        for k in range(3):
+            env.step(iw, k == 0, k == 0)
+        case["stepped"] = snap()
+        case["stepped_env"] = {"sampling_distance_travelled": float(env.sampling_distance_travelled),
+                               "eps_distance_travelled": float(env.eps_distance_travelled)}
+        out["cases"][mode] = case
+    with open(os.path.join(HERE, "asset_paths.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seed", type=int, default=25450)
-    ap.add_argument("--only", choices=("simplified",), help="write only this group of fixtures")
+    ap.add_argument("--only", choices=("simplified", "assets"), help="write only this group of fixtures")
     args = ap.parse_args()
+    if args.only == "assets":
+        gen_asset_paths(*install_env_shims())
+        return
     ref = _import_reference()
     # SimplifiedMachineryModel: PTI from rest with zero thrust (throttle saturated, then regulating
     # 3 m/s), and the collision-biased PTO variant slowing from 6 to 3.5 m/s

@@ -618,8 +618,12 @@ def _rollouts(env, blob, kernel, launches, steps, monkeypatch):
     env.load_state_blob(blob)
     res = []
     for i in range(launches):
-        o = env.rollout(steps, seed=41, transition_capacity=4 * env.n_env, mask_horizon=700)
-        tr = o["transitions"][:int(o["transition_count"].item())].cpu().numpy()
+        # capacity for one event per env-step: nothing is dropped (which records an overflowing buffer
+        # keeps depends on the order of the atomics; PTO / MEC blackouts restart episodes every few steps)
+        o = env.rollout(steps, seed=41, transition_capacity=steps * env.n_env, mask_horizon=700)
+        cnt = int(o["transition_count"].item())
+        assert cnt <= steps * env.n_env
+        tr = o["transitions"][:cnt].cpu().numpy()
         # per env in step order: one wave writes an env's records, each step's slots allocated after the
         # previous step's (a stable sort by env id keeps that order; records of repeated episode starts
         # can tie on every value column)
