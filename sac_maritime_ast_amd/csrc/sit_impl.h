@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1249,8 +1250,9 @@ Consts<T> make_consts(const sit_handle* h) {
   {  // sqrt(x) <= r  <=>  x <= d2_le (IEEE sqrt is correctly rounded and monotone)
     const double r = p.arrival_radius;
     double v = r * r;
-    while (std::sqrt(std::nextafter(v, INFINITY)) <= r) v = std::nextafter(v, INFINITY);
-    while (v > 0 && std::sqrt(v) > r) v = std::nextafter(v, -INFINITY);
+    // (towards +-DBL_MAX, not infinity: the float32 TU's device pass parses this with finite math)
+    while (std::sqrt(std::nextafter(v, DBL_MAX)) <= r) v = std::nextafter(v, DBL_MAX);
+    while (v > 0 && std::sqrt(v) > r) v = std::nextafter(v, -DBL_MAX);
     c.arrive_d2_le = v;
   }
   c.theta = (T)p.theta;

@@ -8,9 +8,12 @@
 // the post-step position is known at the start of the step.  The D wave of each ship publishes it
 // (and the obstacle's IW of the step) before barrier A, then runs guidance, control, machinery and
 // kinetics; meanwhile the ship's P wave evaluates the map predicates of that position (boundary
-// distance, hull in terrain, the IW test; MSRL_env_ex.py:490-542, 628-881).  Barrier B joins them:
-// D decides the episode's end and runs the auto reset, P turns the distance into the reward terms,
-// and P0, one step behind, writes reward / done / status and the replay transition.
+// distance, hull in terrain, the IW test; MSRL_env_ex.py:490-542, 628-881) and every other predicate
+// of a position alone (arrival, map horizon, and P0 the ship-ship collision).  Barrier B joins them:
+// D decides the episode's end and runs the auto reset; P turns its predicates into the reward terms
+// and writes its ship's next_state columns (P1 also the IW action row); P0, one step behind, writes
+// reward / done / status and the replay transition.  The D waves carry the step's serial chain
+// (guidance, control, machinery, kinetics), so everything that needs only a position runs on P.
 //
 // Roles: a 256-thread block is one env group of kSyncLanes envs x {D0, D1, P0, P1}; odd blocks take
 // the roles in mirrored order (P0 P1 D0 D1), which aims each SIMD at one D and one P wave.
@@ -31,10 +34,15 @@
 constexpr int kSyncLanes = SIT_SYNC_LANES;
 static_assert(kSyncLanes >= 1 && kSyncLanes <= kWave, "SIT_SYNC_LANES must be in [1, 64]");
 
-// D-wave flags of a step (kSf*), per ship
-constexpr uint32_t kSfArrive = 1u << 0, kSfHorizon = 1u << 1, kSfNav = 1u << 2, kSfMech = 1u << 3,
-                   kSfEct = 1u << 4, kSfBlk = 1u << 5, kSfStopPre = 1u << 8, kSfDoneNt = 1u << 9,
+// D-wave flags of a step (kSf*), per ship: the predicates of the ship's own step
+constexpr uint32_t kSfNav = 1u << 2, kSfMech = 1u << 3, kSfEct = 1u << 4, kSfBlk = 1u << 5, kSfStopPre = 1u << 8,
                    kSfSac = 1u << 10, kSfOverflow = 1u << 11;
+constexpr uint32_t kSfDone = kSfNav | kSfMech | kSfEct | kSfBlk;   // end the episode
+// P-wave bits of a step (kPb*), per ship: the predicates of the post-step position
+constexpr uint32_t kPbTerrain = 1u << 0, kPbIw = 1u << 1, kPbArrive = 1u << 2, kPbHorizon = 1u << 3,
+                   kPbColl = 1u << 4;   // kPbColl: the ship-ship collision, in the test ship's word (P0)
+// the episode ends: test ship arrival / horizon / terrain; obstacle horizon / terrain / IW; collision
+constexpr uint32_t kPbDoneTest = kPbArrive | kPbHorizon | kPbTerrain | kPbColl, kPbDoneObs = kPbHorizon | kPbTerrain | kPbIw;
 // the step's policy-mode decision (SyncSlot::q): the env steps / it stopped earlier in this launch;
 // q >= 0: it stops at this step and its request went to slot q of the queue
 constexpr int32_t kQLive = -1, kQStalled = -2;
@@ -43,12 +51,13 @@ template <typename T>
 struct SyncSlot {             // one step of the envs of a group (ring of 2)
   T pn[2][kWave], pe[2][kWave];   // post-step position per ship (D, before A)
   T iwn[kWave], iwe[kWave];       // the obstacle's IW of the step (D1, before A)
+  T ang[kWave];                   // the route angle of the step's sampling event (D1, before A)
   int32_t q[kWave];               // policy mode: kQLive / kQStalled / request slot (D1, before A)
   T t[6][kWave];              // test ship: n, e, psi, rpm, |e_ct|, P_me (D0, before B)
   T o[5][kWave];              // obstacle: n, e, psi, |e_ct|, SAC action (D1, before B)
   uint32_t f[2][kWave];       // kSf* flags per ship (D, before B)
   int32_t ep[kWave];          // episode step before the step (D1)
-  uint32_t pb[2][kWave];      // P per ship: bit 0 test terrain, bit 1 obstacle terrain, bit 2 IW terminal (before B)
+  uint32_t pb[2][kWave];      // kPb* bits per ship (P, before B)
   T r_nto[kWave], r_o[kWave]; // P1 after B: the obstacle's reward terms
   uint32_t bo[kWave];         // P1 after B: the obstacle's status bits | stop | done
 };
@@ -124,12 +133,8 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     r0.load_leg(1);
     leg0 = r0.leg();
   }
-  uint32_t uf = __builtin_amdgcn_readfirstlane((a.io.next_state ? 1u : 0u) | (a.io.action_out ? 16u : 0u) |
-                                               (c.collision_bias ? kUfCollBias : 0u) |
+  uint32_t uf = __builtin_amdgcn_readfirstlane((c.collision_bias ? kUfCollBias : 0u) |
                                                (c.sg_mode != SIT_SG_MOTOR ? kUfBlackout : 0u));
-  T* p_ns = (uf & 1) ? a.io.next_state + (size_t)env * SIT_OBS_DIM + (TYPE == 0 ? 0 : 6) : nullptr;
-  T* p_ao = (uf & 16) ? a.io.action_out + (size_t)env * 4 : nullptr;
-  const size_t row_step = (size_t)n_env;
 
   for (int it = 0; it < n; ++it) {
     asm volatile("" : "+s"(uf));
@@ -169,6 +174,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         }
         if (MODE == kPolicy) xd.q[lane] = q;
         xd.iwn[lane] = iwn; xd.iwe[lane] = iwe;
+        xd.ang[lane] = angle_or_nan(sac, (T)ang);
       }
       xd.pn[TYPE][lane] = n1; xd.pe[TYPE][lane] = e1;
     } else if (MODE == kPolicy && TYPE == 1 && act) {
@@ -208,18 +214,14 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
           ppn = pre_n; ppe = pre_e;
           s.ticks += 1;
         }
-        const bool arrive = within_radius(s.n, s.e, rt.end_n, rt.end_e, c.arrive_d2_le);
-        const bool horizon = outside(c, s.n, s.e, c.half_len);
+        // is_obs_ship_navigation_failure (MSRL_env_ex.py:566-576); arrival and the map horizon are
+        // the P wave's (a function of the position)
         const bool nav = ect_over || (double)samp > samp_limit;
-        fl |= (arrive ? kSfArrive : 0u) | (horizon ? kSfHorizon : 0u) | (nav ? kSfNav : 0u) |
-              ((horizon || nav) ? kSfDoneNt : 0u);
-        if (arrive || horizon || nav) s.stop = 1;
+        fl |= nav ? kSfNav : 0u;
         xd.o[0][lane] = s.n; xd.o[1][lane] = s.e; xd.o[2][lane] = s.psi; xd.o[3][lane] = o_ect;
         xd.o[4][lane] = (T)act_n;
         xd.f[1][lane] = fl;
         xd.ep[lane] = ep_step;
-        if (uf & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_ect); }
-        if (uf & 16) { store2(p_ao, iwn, iwe); store2(p_ao + 2, angle_or_nan(sac, (T)ang), sac ? T(1) : T(0)); }
       } else {
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
@@ -243,27 +245,22 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
         ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
         s.ticks += 1;
-        const bool arrive = within_radius(s.n, s.e, rt.end_n, rt.end_e, c.arrive_d2_le);
-        const bool horizon = outside(c, s.n, s.e, c.half_len);
-        const bool any = arrive || horizon || mech || ect_over || blk;
-        fl |= (arrive ? kSfArrive : 0u) | (horizon ? kSfHorizon : 0u) | (mech ? kSfMech : 0u) |
-              (ect_over ? kSfEct : 0u) | (blk ? kSfBlk : 0u) | (any ? kSfDoneNt : 0u);
-        if (any) s.stop = 1;
+        fl |= (mech ? kSfMech : 0u) | (ect_over ? kSfEct : 0u) | (blk ? kSfBlk : 0u);
         xd.t[0][lane] = s.n; xd.t[1][lane] = s.e; xd.t[2][lane] = s.psi;
         xd.t[3][lane] = o_rpm; xd.t[4][lane] = o_ect; xd.t[5][lane] = o_pme;
         xd.f[0][lane] = fl;
-        if (uf & 1) { store2(p_ns, s.n, s.e); store2(p_ns + 2, s.psi, o_rpm); store2(p_ns + 4, o_ect, o_pme); }
       }
     }
     __syncthreads();   // B: both ships' step and their map predicates
     // the episode's end (every predicate, the collision) and the auto reset (main_ast.py:314-333)
     if (act && !stalled) {
-      const T tn = xd.t[0][lane], te = xd.t[1][lane], on = xd.o[0][lane], oe = xd.o[1][lane];
-      const bool coll = closer_than(tn, te, on, oe, c.coll_d2);
-      const bool env_done = ((xd.f[0][lane] | xd.f[1][lane]) & kSfDoneNt) || ((xd.pb[0][lane] | xd.pb[1][lane]) & 7u) ||
-                            coll;
-      if (coll) s.stop = 1;
-      if (TYPE == 1 && (xd.pb[1][lane] & 4u)) s.stop = 1;   // the IW terminal stops the obstacle (Q11)
+      const uint32_t pb0 = xd.pb[0][lane], pb1 = xd.pb[1][lane];
+      const bool env_done = ((xd.f[0][lane] | xd.f[1][lane]) & kSfDone) || (pb0 & kPbDoneTest) || (pb1 & kPbDoneObs);
+      // the stop flags (MSRL_env_ex.py:742-899): the test ship stops with any of its predicates, the
+      // obstacle at arrival, the map horizon, an IW terminal (Q11) and navigation failure, not at the
+      // terrain (Q12); both at a collision.  (A test-ship predicate ends the episode: reset below.)
+      if (TYPE == 0) { if ((xd.f[0][lane] & kSfDone) || (pb0 & kPbDoneTest)) s.stop = 1; }
+      else if ((xd.f[1][lane] & kSfNav) || (pb1 & (kPbArrive | kPbHorizon | kPbIw)) || (pb0 & kPbColl)) s.stop = 1;
       rt.fixup(s.k);
       ep_step += 1;
       if (env_done) {
@@ -277,8 +274,6 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         init_step_ship(c, cs.x, s, rt, v_des);
       }
     }
-    p_ns += row_step * SIT_OBS_DIM;
-    p_ao += row_step * 4;
   }
   __syncthreads();   // C: P1's reward terms of the last step (P0 writes that step's outputs)
   if (act) {
@@ -314,14 +309,22 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     for (int j = 0; j < SIT_OBS_DIM; ++j) lo[j] = a.st.last_obs[(size_t)j * n_env + env];
   T r_nt_t = T(0), r_term_t = T(0); // P0: the test ship's reward terms and bits of the last step
   uint32_t bits_t = 0;
+  bool coll_t = false;              // P0: the last step's ship-ship collision
   T dobst = T(0);
-  bool terrain = false, iw_term = false;
+  uint32_t pbits = 0;               // this step's kPb* predicates of the ship's post-step position
   bool stalled = false;             // policy mode: the env stopped for the policy in this launch
   uint32_t n_stepped = 0;           // policy mode (P0): env-steps executed
-  uint32_t uf = __builtin_amdgcn_readfirstlane((a.io.reward ? 2u : 0u) | (a.io.done ? 4u : 0u) |
-                                               (a.io.status ? 8u : 0u) | (a.io.transitions ? kUfTrans : 0u) |
+  // the ship's final waypoint (the arrival predicate, MSRL_env_ex.py:750-754, 825-829)
+  const T end_n = act ? a.sc.end_n[TYPE * n_env + env] : T(0), end_e = act ? a.sc.end_e[TYPE * n_env + env] : T(0);
+  uint32_t uf = __builtin_amdgcn_readfirstlane((a.io.next_state ? 1u : 0u) | (a.io.reward ? 2u : 0u) |
+                                               (a.io.done ? 4u : 0u) | (a.io.status ? 8u : 0u) |
+                                               (a.io.action_out ? 16u : 0u) | (a.io.transitions ? kUfTrans : 0u) |
                                                (a.io.done_count ? kUfDoneCnt : 0u) |
                                                (a.io.mask_horizon > 0 ? kUfMaskH : 0u));
+  // this ship's next_state columns (P0: 0-5, P1: 6-9) and, P1, the IW action row, one row block per step
+  T* p_ns = (uf & 1) ? a.io.next_state + (size_t)env * SIT_OBS_DIM + (TYPE == 0 ? 0 : 6) : nullptr;
+  T* p_ao = (TYPE == 1 && (uf & 16)) ? a.io.action_out + (size_t)env * 4 : nullptr;
+  const size_t row_step = (size_t)n_env;
 
   // P0: reward, done, status, replay transition and done count of step j (MSRL_env_ex.py:906-980)
   auto outputs = [&](int j) {
@@ -343,7 +346,7 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     }
     if (live) {
       const T tn = xd.t[0][lane], te = xd.t[1][lane], on = xd.o[0][lane], oe = xd.o[1][lane];
-      const bool coll = closer_than(tn, te, on, oe, c.coll_d2);
+      const bool coll = coll_t;
       const uint32_t bo = xd.bo[lane];
       env_done = (bits_t & SIT_ST_TEST_DONE) || (bo & kDoneBit) || coll;
       const T dn = tn - on, de = te - oe;
@@ -397,25 +400,30 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     __syncthreads();   // A: this step's positions
     if (TYPE == 0 && it >= 1) outputs(it - 1);
     if (MODE == kPolicy && act && !stalled) stalled = xd.q[lane] != kQLive;
-    // the map predicates of the post-step position (MSRL_env_ex.py:490-542, 628-881)
+    // the predicates of the post-step position (MSRL_env_ex.py:460-603, 628-881): the map's (boundary
+    // distance, hull in terrain, the IW test), arrival within 200 m of the final waypoint, the map
+    // horizon, and (P0) the ship-ship collision
     if (act && !stalled) {
       const T sn = xd.pn[TYPE][lane], se = xd.pe[TYPE][lane];
       DistPf<T> pf;
       pf_cell(c, map, sn, se, pf);
       pf_edges(map, pf);
       dobst = pf_finish(map, pf, sn, se);
-      terrain = hull_in_terrain_cls(c, map, sn, se, dobst, pf.cls, pf.cell_f, pf.word_f);
+      const bool terrain = hull_in_terrain_cls(c, map, sn, se, dobst, pf.cls, pf.cell_f, pf.word_f);
+      pbits = (terrain ? kPbTerrain : 0u) | (within_radius(sn, se, end_n, end_e, c.arrive_d2_le) ? kPbArrive : 0u) |
+              (outside(c, sn, se, c.half_len) ? kPbHorizon : 0u);
       if (TYPE == 1) {
         const T wn = xd.iwn[lane], we = xd.iwe[lane];
         if (!iw_valid || wn != iw_tn || we != iw_te) {
           iw_in = pip_point(c, map, wn, we);
           iw_tn = wn; iw_te = we; iw_valid = true;
         }
-        iw_term = outside(c, wn, we, T(0)) || iw_in;   // Q11
-        xd.pb[1][lane] = (terrain ? 2u : 0u) | (iw_term ? 4u : 0u);
+        if (outside(c, wn, we, T(0)) || iw_in) pbits |= kPbIw;   // Q11
       } else {
-        xd.pb[0][lane] = terrain ? 1u : 0u;
+        coll_t = closer_than(sn, se, xd.pn[1][lane], xd.pe[1][lane], c.coll_d2);   // MSRL_env_ex.py:584-603
+        if (coll_t) pbits |= kPbColl;
       }
+      xd.pb[TYPE][lane] = pbits;
     }
     __syncthreads();   // B: the D waves' step results
     if (act && !stalled) {
@@ -424,9 +432,15 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       bool done = false;
       T r_nt = T(0), r_term = T(0);
       uint32_t bits = 0;
+      const bool terrain = (pbits & kPbTerrain) != 0;
       if (TYPE == 0) {
-        r_nt = xabs(xd.t[4][lane]) * c.inv_e_tol + (T(1) - dobst * c.inv_maxn) * T(0.01);
-        const bool pred[6] = {(fl & kSfArrive) != 0, (fl & kSfHorizon) != 0, terrain, (fl & kSfMech) != 0,
+        const T t4 = xd.t[4][lane];
+        if (uf & 1) {                    // next_state columns 0-5 (MSRL_Env.py:426-437)
+          store2(p_ns, xd.t[0][lane], xd.t[1][lane]); store2(p_ns + 2, xd.t[2][lane], xd.t[3][lane]);
+          store2(p_ns + 4, t4, xd.t[5][lane]);
+        }
+        r_nt = xabs(t4) * c.inv_e_tol + (T(1) - dobst * c.inv_maxn) * T(0.01);
+        const bool pred[6] = {(pbits & kPbArrive) != 0, (pbits & kPbHorizon) != 0, terrain, (fl & kSfMech) != 0,
                               (fl & kSfEct) != 0, (fl & kSfBlk) != 0};
         const T rew[6] = {T(0), T(0), T(1000), T(1000), T(1000), T(1000)};
 #pragma unroll
@@ -441,17 +455,23 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
         if (done) bits |= SIT_ST_TEST_DONE;
         r_nt_t = r_nt; r_term_t = r_term; bits_t = bits;
       } else {
+        const T o3 = xd.o[3][lane];
+        if (uf & 1) { store2(p_ns, xd.o[0][lane], xd.o[1][lane]); store2(p_ns + 2, xd.o[2][lane], o3); }
+        if (uf & 16) {                   // the IW action row: north, east, route angle, SAC_update
+          const bool sac = (fl & kSfSac) != 0;
+          store2(p_ao, xd.iwn[lane], xd.iwe[lane]); store2(p_ao + 2, xd.ang[lane], sac ? T(1) : T(0));
+        }
         if (!stop)
-          r_nt = T(0.1) - xabs(xd.o[3][lane]) * c.inv_e_tol * T(0.01) - (T(1) - dobst * c.inv_maxn) * T(0.01);
+          r_nt = T(0.1) - xabs(o3) * c.inv_e_tol * T(0.01) - (T(1) - dobst * c.inv_maxn) * T(0.01);
         bits = (fl & kSfOverflow) ? SIT_ST_ROUTE_OVERFLOW : 0u;
-        if (fl & kSfArrive) { stop = 1; bits |= SIT_ST_OBS_ENDPOINT; }
-        if (fl & kSfHorizon) { stop = 1; done = true; bits |= SIT_ST_OBS_HORIZON; }
+        if (pbits & kPbArrive) { stop = 1; bits |= SIT_ST_OBS_ENDPOINT; }
+        if (pbits & kPbHorizon) { stop = 1; done = true; bits |= SIT_ST_OBS_HORIZON; }
         if (terrain) {                   // done without stop flag (Q12)
           if (!stop) r_term = r_term - T(1000);
           done = true;
           bits |= SIT_ST_OBS_TERRAIN;
         }
-        if (iw_term) {
+        if (pbits & kPbIw) {
           if (!stop) r_term = r_term - T(1000);
           stop = 1; done = true;
           bits |= SIT_ST_OBS_IW_TERMINAL;
@@ -467,6 +487,8 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
         xd.bo[lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u);
       }
     }
+    p_ns += row_step * SIT_OBS_DIM;
+    p_ao += row_step * 4;
   }
   __syncthreads();   // C
   if (TYPE == 0) {
