@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="rollout mode: skip the config C5 (policy) line")
     ap.add_argument("--c5-steps", type=int, default=32 * 16 * 16, help="timed steps of the C5 line")
     ap.add_argument("--c5-warmup", type=int, default=32 * 16 * 60, help="warm-up steps of the C5 line")
+    ap.add_argument("--c5-groups", type=int, default=1, help="C5 line: stream groups (1 measured fastest)")
+    ap.add_argument("--c5-chunk", type=int, default=64, help="C5 line: env steps per launch")
     args = ap.parse_args()
     if args.chunk is None:
         args.chunk = 32 if args.mode == "policy" else 40000
@@ -585,8 +587,8 @@ def main():
     if args.mode == "rollout" and not args.no_c5:
         # config C5 beside the headline C3/C4 line: policy mode, driver-timed in the same run
         a5 = argparse.Namespace(**vars(args))
-        a5.mode, a5.chunk = "policy", 32
-        a5.steps, a5.warmup = max(args.c5_steps, 32 * 16 * 2), args.c5_warmup
+        a5.mode, a5.chunk, a5.groups = "policy", args.c5_chunk, args.c5_groups
+        a5.steps, a5.warmup = max(args.c5_steps, a5.chunk * 16 * 2), args.c5_warmup
         c5 = bench_policy(a5, rank, world, dev)
     result = {"metric": METRIC, "value": r["value"], "unit": "env-steps/s", "n_gpus": world, "steps": r["steps"],
               "warmup": r["warmup"], "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",

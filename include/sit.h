@@ -269,6 +269,14 @@ int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint
  * compiled with the float32 step kernels' fast-math flags.  Device pointers. */
 int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, double* out, int32_t fast_tu,
                      void* stream);
+/* Debug builds (libsit_debug.so, compiled with -DSIT_DEBUG; no reference counterpart): every table
+ * index the step kernels compute is bounds-checked; a failed check sets bit i of the returned word
+ * (0 route-table row, 1 next-waypoint index, 2 route length, 3 spatial-index entry, 4 edge id,
+ * 5 class-grid word, 6 mixed-cell record, 7 ship index) and its access is clamped into the table, so
+ * the launch completes.  sit_debug_flags synchronises the device, returns the bits set since the last
+ * call and clears them; release builds return 0.  sit_debug_build: 1 in a debug build. */
+int sit_debug_flags(uint32_t* flags);
+int32_t sit_debug_build(void);
 /* Put every env into its construction-time state (as if freshly built).  Unlike
  * sit_reset this also re-initialises the shaft speed and all controller integrators. */
 int sit_restart(sit_handle* h, void* stream);

@@ -89,6 +89,39 @@ __device__ __forceinline__ double ieee_dot2(double x, double y, double z, double
   return ieee_add(ieee_mul(x, y), ieee_mul(z, w));
 }
 
+// Debug builds (-DSIT_DEBUG, libsit_debug.so; SURVEY §5: bounds asserts in a debug kernel variant):
+// every table index the step computes is checked before use.  A failed check sets its bit in
+// g_dbg_flags (one word per translation unit, read and cleared by sit_debug_flags) instead of
+// trapping, and the index is clamped into its table: the launch completes without touching memory
+// out of bounds and the host reports which check failed.  Release builds compile the checks out.
+enum DebugCheck {
+  kDbgRouteIndex = 0,    // a route-table row outside [0, wpt_capacity)
+  kDbgWaypoint = 1,      // the next-waypoint index k outside [1, n_wpt)
+  kDbgRouteLen = 2,      // a route length outside [2, wpt_capacity]
+  kDbgIndexEntry = 3,    // a grid / band entry outside the packed spatial index
+  kDbgEdgeId = 4,        // an edge id >= the map's edge count
+  kDbgClassWord = 5,     // a class-grid word outside the grid
+  kDbgCellRecord = 6,    // a mixed-cell record or live-edge entry outside its table
+  kDbgShip = 7,          // a ship / env index outside the handle's population
+};
+#ifdef SIT_DEBUG
+namespace {
+__device__ unsigned int g_dbg_flags;
+}
+__device__ __forceinline__ int dbg_clamp(int i, int n, int id) {
+  if (i < 0 || i >= n) {
+    atomicOr(&g_dbg_flags, 1u << id);
+    return 0;
+  }
+  return i;
+}
+#define SIT_DCHECK(cond, id) do { if (!(cond)) atomicOr(&::sit::g_dbg_flags, 1u << (id)); } while (0)
+#define SIT_DCLAMP(i, n, id) ::sit::dbg_clamp((i), (n), (id))
+#else
+#define SIT_DCHECK(cond, id) do { } while (0)
+#define SIT_DCLAMP(i, n, id) (i)
+#endif
+
 constexpr int kWave = 64;         // CDNA wavefront
 #ifndef SIT_ENVS_PER_BLOCK
 #define SIT_ENVS_PER_BLOCK 64
@@ -251,6 +284,7 @@ struct Map {
   const uint2* crec;
   const uint8_t* clive;
   int32_t use_cells;
+  int32_t n_idx, n_mixed, n_live;   // entries of idx / crec / clive (bounds of the debug checks)
   // fallback scan (global memory): polygon ring offsets and bounding boxes
   const int32_t* off;       // [n_poly + 1]
   const T* bbox;            // [n_poly][4] min_x, max_x, min_y, max_y
@@ -324,6 +358,7 @@ struct Route {
   T* tn;          // column base: entry i at tn[i * stride]
   T* te;
   int stride;
+  int cap;        // table rows (wpt_capacity)
   T end_n, end_e;
   int nw;         // current number of waypoints
   T pn, pe;       // waypoint k-1
@@ -338,11 +373,11 @@ struct Route {
   // unconditionally at min(i, nw - 1) (inside the column: nw <= capacity), so a leg's loads issue
   // together instead of behind one branch each (one memory round trip per leg reload)
   __device__ __forceinline__ T n(int i) const {
-    const T v = tn[(i < nw - 1 ? i : nw - 1) * stride];
+    const T v = tn[SIT_DCLAMP(i < nw - 1 ? i : nw - 1, cap, kDbgRouteIndex) * stride];
     return (i >= nw - 1) ? end_n : v;
   }
   __device__ __forceinline__ T e(int i) const {
-    const T v = te[(i < nw - 1 ? i : nw - 1) * stride];
+    const T v = te[SIT_DCLAMP(i < nw - 1 ? i : nw - 1, cap, kDbgRouteIndex) * stride];
     return (i >= nw - 1) ? end_e : v;
   }
   __device__ __forceinline__ void load_next(int k) {
@@ -350,6 +385,8 @@ struct Route {
     leg_geom(cn, ce, nn, ne, alpha_n, sa_n, ca_n);
   }
   __device__ __forceinline__ void load_leg(int k) {
+    SIT_DCHECK(nw >= 2 && nw <= cap, kDbgRouteLen);
+    SIT_DCHECK(k >= 1 && k < nw, kDbgWaypoint);
     pn = n(k - 1); pe = e(k - 1); cn = n(k); ce = e(k);
     leg_geom(pn, pe, cn, ce, alpha, sa, ca);
     load_next(k);
@@ -831,6 +868,7 @@ __device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   uint2 q = reinterpret_cast<const uint2*>(m.idx)[cell];
   const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (q.y >> 16);
   const int ng = (int)((q.y >> 8) & 0xffu);
+  SIT_DCHECK(4 * ((int)(q.y >> 16) + ng) <= m.n_idx, kDbgIndexEntry);
   T best = xmin(xmin(xmin(edge_dist2(m.edge[q.x & 0xffu], e, n), edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n)),
                      xmin(edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n), edge_dist2(m.edge[q.x >> 24], e, n))),
                 edge_dist2(m.edge[q.y & 0xffu], e, n));
@@ -872,6 +910,9 @@ __device__ __forceinline__ void pf_cell(const Consts<T>& c, const Map<T>& m, T n
 }
 template <typename T>
 __device__ __forceinline__ void pf_edges(const Map<T>& m, DistPf<T>& p) {
+  SIT_DCHECK((int)(p.q.x & 0xffu) < m.n_edge && (int)((p.q.x >> 8) & 0xffu) < m.n_edge &&
+             (int)((p.q.x >> 16) & 0xffu) < m.n_edge && (int)(p.q.x >> 24) < m.n_edge &&
+             (int)(p.q.y & 0xffu) < m.n_edge, kDbgEdgeId);
   p.g[0] = m.edge[p.q.x & 0xffu];
   p.g[1] = m.edge[(p.q.x >> 8) & 0xffu];
   p.g[2] = m.edge[(p.q.x >> 16) & 0xffu];
@@ -883,12 +924,15 @@ __device__ __forceinline__ T pf_finish(const Map<T>& m, const DistPf<T>& p, T n,
   if (!p.ok) return distance_to_polys(m, n, e);
   const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (p.q.y >> 16);
   const int ng = (int)((p.q.y >> 8) & 0xffu);
+  SIT_DCHECK(4 * ((int)(p.q.y >> 16) + ng) <= m.n_idx, kDbgIndexEntry);
   T best = xmin(xmin(xmin(edge_dist2(p.g[0], e, n), edge_dist2(p.g[1], e, n)),
                      xmin(edge_dist2(p.g[2], e, n), edge_dist2(p.g[3], e, n))),
                 edge_dist2(p.g[4], e, n));
 #pragma unroll 1
   for (int g = 0; g < ng; ++g) {
     const uint2 q = grp[g];
+    SIT_DCHECK((int)(q.x & 0xffu) < m.n_edge && (int)(q.x >> 24) < m.n_edge && (int)(q.y & 0xffu) < m.n_edge,
+               kDbgEdgeId);
     const T d0 = edge_dist2(m.edge[q.x & 0xffu], e, n);
     const T d1 = edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n);
     const T d2 = edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n);
@@ -909,6 +953,7 @@ __device__ int pip_pair_indexed(const Consts<T>& c, const Map<T>& m, double n, d
   const int b = (int)fb;
   uint32_t par0 = 0, onb0 = 0, par1 = 0, onb1 = 0;
   const int k0 = m.idx[kBandBase + b], k1 = m.idx[kBandBase + b + 1];
+  SIT_DCHECK(k0 <= k1 && k1 <= m.n_idx, kDbgIndexEntry);
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
     const Edge<T> g = m.edge[m.idx[k]];
@@ -945,7 +990,7 @@ __device__ __forceinline__ int fine_lookup(const Consts<T>& c, const Map<T>& m, 
   word = 0;
   if (!(fx >= T(0) && fx < T(kFine) && fy >= T(0) && fy < T(kFine))) return 0;
   cell = (int)fy * kFine + (int)fx;
-  word = m.fine[cell >> 4];
+  word = m.fine[SIT_DCLAMP(cell >> 4, kFineWords, kDbgClassWord)];
   return (word >> ((cell & 15) * 2)) & 3;
 }
 
@@ -1010,9 +1055,11 @@ constexpr int kPipExact = 2;   // no distance known (the IW point, probes): floa
 template <int MODE, typename T>
 __device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t word, T n, T e, double nd, double ed) {
   const uint32_t mixed = (word >> 1) & 0x55555555u;
-  const int r = m.frank[cell >> 4] + __popc(mixed & ((1u << ((cell & 15) * 2)) - 1u));
+  const int r = SIT_DCLAMP(m.frank[cell >> 4] + __popc(mixed & ((1u << ((cell & 15) * 2)) - 1u)), m.n_mixed,
+                           kDbgCellRecord);
   const uint2 rec = m.crec[r];
   const int first = (int)(rec.y & 0xffffu), cnt = (int)(rec.y >> 16);
+  SIT_DCHECK(first + cnt <= m.n_live, kDbgCellRecord);
   if constexpr (kIsF32<T> && MODE == kPipFar) {
     uint32_t par = rec.x, onb = 0;
 #pragma unroll 1

@@ -180,6 +180,18 @@ namespace {   // kernels are TU-local: the float32 step kernels live in their ow
 // ---------------------------------------------------------------------------------------
 // device helpers on the SoA state
 // ---------------------------------------------------------------------------------------
+#ifdef SIT_DEBUG
+// this translation unit's failed bounds checks (sit_debug_flags), read and cleared
+int debug_flags_impl(uint32_t* out) {
+  unsigned int v = 0, z = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return SIT_E_HIP;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(sit::g_dbg_flags), sizeof(v)) != hipSuccess) return SIT_E_HIP;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(sit::g_dbg_flags), &z, sizeof(z)) != hipSuccess) return SIT_E_HIP;
+  *out |= v;
+  return SIT_OK;
+}
+#endif
+
 template <typename T>
 __device__ __forceinline__ void load_ship(const State<T>& st, int sid, Ship<T>& s) {
   s.n = st.ship[0][sid]; s.e = st.ship[1][sid]; s.psi = st.ship[2][sid];
@@ -276,10 +288,22 @@ __device__ __forceinline__ double angle_or_nan(bool has, double a) {
 //           sampling event without a fresh action waits for the rest of the launch and queues
 //           a request; the next launch consumes the action the policy wrote for it)
 // ---------------------------------------------------------------------------------------
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
-// Diagnostic builds only (tools/diag_paths.py): [type][0..15] predicate path statistics,
-// [type][16..23] shader-clock cycles per step phase (wave lane 0).
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC)
+// Diagnostic builds only (tools/diag_paths.py, tools/diag_sync.py): [type][0..15] predicate path
+// statistics, [type][16..23] shader-clock cycles per step phase (wave lane 0); SIT_DIAG_SYNC: cycles
+// per role and segment of k_env_steps_sync (sit_sync.h).  The counters are per translation unit:
+// sit_diag_read reads the float64 TU's, sit_diag_read_f32 the float32 step kernels'.
 __device__ unsigned long long g_sit_diag[2][32];
+int diag_read_impl(unsigned long long* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sit_diag), sizeof(g_sit_diag)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[2][32] = {};
+    for (int t = 0; t < 2; ++t) z[t][28] = z[t][30] = ~0ull;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sit_diag), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
 #endif
 #ifdef SIT_DIAG_PHASES
 // per wave of the last launch: start / end (realtime ticks), shader cycles, HW_ID | XCC_ID << 32
@@ -464,6 +488,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
     rt.tn = a.st.wn + (size_t)type * a.cap * n_env + env;
     rt.te = a.st.we + (size_t)type * a.cap * n_env + env;
     rt.stride = n_env;
+    rt.cap = a.cap;
     rt.load_leg(s.k);
     if (type == 1) {
       samp = a.st.env[0][env]; eps = a.st.env[1][env];
@@ -965,6 +990,7 @@ __global__ __launch_bounds__(256) void k_init_step(const KArgs<T> a, const uint8
   rt.tn = a.st.wn + (size_t)type * a.cap * n_env + env;
   rt.te = a.st.we + (size_t)type * a.cap * n_env + env;
   rt.stride = n_env;
+  rt.cap = a.cap;
   rt.load_leg(s.k);
   init_step_ship(a.c, a.c.x, s, rt, init_val(a.sc, type, SIT_INIT_DESIRED_SPEED, env, n_env));
   store_ship(a.st, sid, s);
@@ -1103,7 +1129,7 @@ struct sit_handle {
   int n_poly = 0, n_vert = 0;
   size_t map_idx = 0, map_fine = 0, map_off = 0, map_bbox = 0, map_frank = 0, map_crec = 0, map_clive = 0;
   int use_cells = 0;
-  int64_t n_mixed = 0, n_live = 0;
+  int64_t n_mixed = 0, n_live = 0, n_idx = 0;
   int lds_attr[24] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
                       -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
@@ -1328,6 +1354,9 @@ KArgs<T> make_args(const sit_handle* h) {
   a.map.crec = reinterpret_cast<const uint2*>(h->map + h->map_crec);
   a.map.clive = reinterpret_cast<const uint8_t*>(h->map + h->map_clive);
   a.map.use_cells = h->use_cells;
+  a.map.n_idx = (int32_t)h->n_idx;
+  a.map.n_mixed = (int32_t)h->n_mixed;
+  a.map.n_live = (int32_t)h->n_live;
   a.map.off = reinterpret_cast<const int32_t*>(h->map + h->map_off);
   a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
   a.map_bytes = (int32_t)h->map_bytes;

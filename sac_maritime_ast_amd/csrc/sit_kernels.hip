@@ -12,6 +12,9 @@ int sit_launch_steps_f32(sit_handle* h, const void* io, void* stream);   // sit_
 int sit_launch_probe_f32(sit_handle* h, int n, const void* pts_ne, void* dist, uint8_t* inside, uint8_t* hull,
                          void* stream);
 int sit_launch_selftest_f32tu(int op, int n, const double* a, const double* b, double* out, void* stream);
+#ifdef SIT_DEBUG
+int sit_debug_flags_f32tu(uint32_t* out);
+#endif
 namespace {
 int launch_steps_f32(sit_handle* h, const StepIO<float>& io, void* stream) {
   return sit_launch_steps_f32(h, &io, stream);
@@ -41,7 +44,7 @@ int launch_selftest_f32tu(int op, int n, const double* a, const double* b, doubl
 // =======================================================================================
 extern "C" {
 
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES)
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC)
 #ifdef SIT_DIAG_PHASES
 int sit_diag_read_waves(unsigned long long* out, int n) {   // [n][4], diagnostic builds only
   if (hipDeviceSynchronize() != hipSuccess) return -1;
@@ -50,16 +53,7 @@ int sit_diag_read_waves(unsigned long long* out, int n) {   // [n][4], diagnosti
   return 0;
 }
 #endif
-int sit_diag_read(unsigned long long* out, int reset) {   // diagnostic builds only
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sit_diag), sizeof(g_sit_diag)) != hipSuccess) return -1;
-  if (reset) {
-    unsigned long long z[2][32] = {};
-    for (int t = 0; t < 2; ++t) z[t][28] = z[t][30] = ~0ull;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sit_diag), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
+int sit_diag_read(unsigned long long* out, int reset) { return diag_read_impl(out, reset); }   // diagnostic builds only
 #endif
 
 int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint8_t* inside, uint8_t* hull,
@@ -130,6 +124,26 @@ int sit_map_info(const sit_handle* h, int64_t* info, int32_t n) {
 }
 
 int32_t sit_abi_version(void) { return SIT_ABI_VERSION; }
+
+#ifdef SIT_DEBUG
+int32_t sit_debug_build(void) { return 1; }
+#else
+int32_t sit_debug_build(void) { return 0; }
+#endif
+
+int sit_debug_flags(uint32_t* flags) {
+  if (!flags) return SIT_E_INVALID;
+  *flags = 0;
+#ifdef SIT_DEBUG
+  int rc = debug_flags_impl(flags);
+#ifdef SIT_F32_TU
+  if (rc == SIT_OK) rc = sit_debug_flags_f32tu(flags);
+#endif
+  return rc;
+#else
+  return SIT_OK;
+#endif
+}
 size_t sit_rollout_args_size(void) { return sizeof(sit_rollout_args); }
 size_t sit_params_size(void) { return sizeof(sit_params); }
 
@@ -478,6 +492,7 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
   h->gx0 = gx0; h->gy0 = gy0; h->ginvx = 1.0 / sx; h->ginvy = 1.0 / sy;
   h->by0 = by0; h->binv = 1.0 / bh;
   std::vector<uint16_t> idx(h->use_index ? n_idx : 4, 0);
+  h->n_idx = (int64_t)idx.size();
   if (h->use_index) {
     for (int c = 0; c < kGrid * kGrid; ++c) {
       const uint16_t* f = gentries.data() + gstart[c];

@@ -21,3 +21,13 @@ int sit_launch_probe_f32(sit_handle* h, int n, const void* pts_ne, void* dist, u
 int sit_launch_selftest_f32tu(int op, int n, const double* a, const double* b, double* out, void* stream) {
   return launch_selftest(op, n, a, b, out, (hipStream_t)stream);
 }
+
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC)
+// diagnostic builds only: this TU's counters (the float32 step kernels')
+extern "C" int sit_diag_read_f32(unsigned long long* out, int reset) { return diag_read_impl(out, reset); }
+#endif
+
+#ifdef SIT_DEBUG
+// the float32 step kernels' failed bounds checks (sit_debug_flags)
+int sit_debug_flags_f32tu(uint32_t* out) { return debug_flags_impl(out); }
+#endif

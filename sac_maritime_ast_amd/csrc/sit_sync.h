@@ -32,6 +32,24 @@
 #define SIT_SYNC_CREF 1     // D waves read the constants from their LDS copy (no VGPR spills; +2.5 %)
 #endif
 constexpr int kSyncLanes = SIT_SYNC_LANES;
+
+// SIT_DIAG_SYNC (diagnostic builds only, tools/diag_sync.py): shader cycles per role and loop segment,
+// lane 0 of each wave, summed into g_sit_diag[role >> 1][(role & 1) * 8 + segment]: 0 work before
+// barrier A, 1 wait at A, 2 work A -> B, 3 wait at B, 4 work after B, 5 wave-steps, 6 P0's outputs
+// of the previous step (part of 2)
+#ifdef SIT_DIAG_SYNC
+#define SY_INIT() unsigned long long sy_t = __builtin_amdgcn_s_memtime(), sy_acc[7] = {0, 0, 0, 0, 0, 0, 0}
+#define SY_MARK(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    sy_acc[k] += t_ - sy_t; sy_t = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#define SY_STEP() (sy_acc[5] += 1)
+#define SY_FLUSH(role) do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 7; ++q_) \
+    atomicAdd(&g_sit_diag[(role) >> 1][((role) & 1) * 8 + q_], sy_acc[q_]); } while (0)
+#else
+#define SY_INIT() do { } while (0)
+#define SY_MARK(k) do { } while (0)
+#define SY_STEP() do { } while (0)
+#define SY_FLUSH(role) do { } while (0)
+#endif
 static_assert(kSyncLanes >= 1 && kSyncLanes <= kWave, "SIT_SYNC_LANES must be in [1, 64]");
 
 // D-wave flags of a step (kSf*), per ship: the predicates of the ship's own step
@@ -136,6 +154,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   uint32_t uf = __builtin_amdgcn_readfirstlane((c.collision_bias ? kUfCollBias : 0u) |
                                                (c.sg_mode != SIT_SG_MOTOR ? kUfBlackout : 0u));
 
+  SY_INIT();
   for (int it = 0; it < n; ++it) {
     asm volatile("" : "+s"(uf));
     SyncSlot<T>& xd = X.d[it & 1];
@@ -180,7 +199,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     } else if (MODE == kPolicy && TYPE == 1 && act) {
       xd.q[lane] = kQStalled;
     }
+    SY_MARK(0);
     __syncthreads();   // A: positions (and the IW, and in policy mode the step's decision) published
+    SY_MARK(1);
     if (MODE == kPolicy && TYPE == 0 && act && !stalled) stalled = xd.q[lane] != kQLive;
     if (act && !stalled) {
       T o_rpm, o_ect, o_pme = T(0);
@@ -251,7 +272,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         xd.f[0][lane] = fl;
       }
     }
+    SY_MARK(2);
     __syncthreads();   // B: both ships' step and their map predicates
+    SY_MARK(3);
     // the episode's end (every predicate, the collision) and the auto reset (main_ast.py:314-333)
     if (act && !stalled) {
       const uint32_t pb0 = xd.pb[0][lane], pb1 = xd.pb[1][lane];
@@ -274,7 +297,10 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         init_step_ship(c, cs.x, s, rt, v_des);
       }
     }
+    SY_MARK(4);
+    SY_STEP();
   }
+  SY_FLUSH(TYPE);
   __syncthreads();   // C: P1's reward terms of the last step (P0 writes that step's outputs)
   if (act) {
     store_ship(a.st, sid, s);
@@ -393,12 +419,16 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     }
   };
 
+  SY_INIT();
   for (int it = 0; it < n; ++it) {
     asm volatile("" : "+s"(uf));
     asm volatile("" : "+s"(map.use_index), "+s"(map.use_cells), "+s"(map.n_edge), "+s"(map.n_poly));
     SyncSlot<T>& xd = X.d[it & 1];
+    SY_MARK(0);
     __syncthreads();   // A: this step's positions
+    SY_MARK(1);
     if (TYPE == 0 && it >= 1) outputs(it - 1);
+    SY_MARK(6);
     if (MODE == kPolicy && act && !stalled) stalled = xd.q[lane] != kQLive;
     // the predicates of the post-step position (MSRL_env_ex.py:460-603, 628-881): the map's (boundary
     // distance, hull in terrain, the IW test), arrival within 200 m of the final waypoint, the map
@@ -425,7 +455,9 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       }
       xd.pb[TYPE][lane] = pbits;
     }
+    SY_MARK(2);
     __syncthreads();   // B: the D waves' step results
+    SY_MARK(3);
     if (act && !stalled) {
       const uint32_t fl = xd.f[TYPE][lane];
       int stop = (fl & kSfStopPre) ? 1 : 0;
@@ -489,7 +521,10 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     }
     p_ns += row_step * SIT_OBS_DIM;
     p_ao += row_step * 4;
+    SY_MARK(4);
+    SY_STEP();
   }
+  SY_FLUSH(2 + TYPE);
   __syncthreads();   // C
   if (TYPE == 0) {
     if (n >= 1) outputs(n - 1);

@@ -696,3 +696,36 @@ def test_sync_kernel_equals_classic(precision, config, monkeypatch):
     print(f"sync vs classic f{precision} {config}: {n_terr} terrain/IW terminations, bitwise {bitwise}, "
           f"worst {dict((k, f'{v:.1e}') for k, v in worst.items())}")
     assert n_terr > 0 or precision == 32, "the case exercises no terrain / IW termination"
+
+
+def test_c4_last_shard_full_size():
+    """The last of config C4's eight shards at its full per-GPU size, as bench.py --gpus 8 runs it on
+    rank 7: envs [7 x 32 768, 8 x 32 768) (scenario and sampler keyed by global env id), one
+    40 000-step float32 launch with the replay transitions at the bench's capacity.  No record is
+    dropped, the done counts equal the done rows, the outputs are finite, and the shard's first 64
+    envs step exactly as a 64-env handle of the same global ids."""
+    n, off, K = 32768, 7 * 32768, 40000
+    env = VecMultiShipRLEnv(scenario=make_scenario(n, cap=48, env_offset=off), precision=32, device=DEV)
+    env.reset()
+    env.init_step()
+    cap = max(n, n * K // 192)                        # bench.py bench_rollout's capacity
+    out = env.rollout(K, seed=25450, env_id_offset=off, transition_capacity=cap)
+    torch.cuda.synchronize()
+    cnt = int(out["transition_count"].item())
+    assert 0 < cnt <= cap, f"{cnt} transitions for capacity {cap}"
+    assert torch.equal(out["done_count"].to(torch.int64), out["done"].to(torch.int64).sum(1))
+    assert int(out["done_count"].sum().item()) > n     # every env ended at least one episode
+    assert bool(torch.isfinite(out["reward"]).all())
+    for k0 in range(0, K, 10000):                     # (in slices: the full array is 52 GB)
+        assert bool(torch.isfinite(out["next_state"][k0:k0 + 10000]).all())
+    tr = out["transitions"][:cnt]
+    ids = tr[:, 23].to(torch.int64)
+    assert int(ids.min()) >= off and int(ids.max()) < off + n
+    head = {k: out[k][:200, :64].cpu().numpy() for k in ("next_state", "reward", "status")}
+    del out
+    small = VecMultiShipRLEnv(scenario=make_scenario(64, cap=48, env_offset=off), precision=32, device=DEV)
+    small.reset()
+    small.init_step()
+    o = small.rollout(200, seed=25450, env_id_offset=off)
+    for k in head:
+        assert np.array_equal(o[k].cpu().numpy(), head[k]), k
