@@ -331,8 +331,17 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   T iw_tn = T(0), iw_te = T(0);     // P1: the IW test's cache (the IW changes at sampling events)
   bool iw_valid = false, iw_in = false;
   T lo[SIT_OBS_DIM] = {};           // P0: the observation before the step (replay transition)
+  // P0: the episode's initial observation, held in registers: a load of it inside the loop left a
+  // global load pending on lo's registers, and the next step's LDS reads into them waited for every
+  // outstanding memory operation (s_waitcnt vmcnt(0)), the step's output stores included (~1 000 cycles)
+  T li[SIT_OBS_DIM] = {};
   if (TYPE == 0 && act)
-    for (int j = 0; j < SIT_OBS_DIM; ++j) lo[j] = a.st.last_obs[(size_t)j * n_env + env];
+    for (int j = 0; j < SIT_OBS_DIM; ++j) {
+      lo[j] = a.st.last_obs[(size_t)j * n_env + env];
+      li[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
+    }
+  // (drained here, so that no load is pending on li's registers when the loop first reads them)
+  __builtin_amdgcn_s_waitcnt(0);
   T r_nt_t = T(0), r_term_t = T(0); // P0: the test ship's reward terms and bits of the last step
   uint32_t bits_t = 0;
   bool coll_t = false;              // P0: the last step's ship-ship collision
@@ -352,7 +361,15 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   T* p_ao = (TYPE == 1 && (uf & 16)) ? a.io.action_out + (size_t)env * 4 : nullptr;
   const size_t row_step = (size_t)n_env;
 
-  // P0: reward, done, status, replay transition and done count of step j (MSRL_env_ex.py:906-980)
+  // P0's output rows, one row per step: per-lane pointers advanced by n_env (kernel-argument pointers
+  // reloaded inside the loop cost a scalar load and its wait per store)
+  T* p_rw = (TYPE == 0 && (uf & 2)) ? a.io.reward + env : nullptr;
+  uint8_t* p_dn = (TYPE == 0 && (uf & 4)) ? a.io.done + env : nullptr;
+  uint32_t* p_st = (TYPE == 0 && (uf & 8)) ? a.io.status + env : nullptr;
+  int* p_dc = (TYPE == 0 && (uf & kUfDoneCnt)) ? a.io.done_count : nullptr;
+
+  // P0: reward, done, status, replay transition and done count of step j (MSRL_env_ex.py:906-980);
+  // called once per step, in order
   auto outputs = [&](int j) {
     const SyncSlot<T>& xd = X.d[j & 1];
     bool env_done = false;
@@ -361,9 +378,8 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       const int32_t q = xd.q[lane];
       live = q == kQLive;
       if (!live) {                     // no step in this row: the env waits for its action
-        const size_t row = (size_t)j * n_env + env;
-        if (uf & 8) a.io.status[row] = SIT_ST_NO_STEP;
-        if (uf & 4) a.io.done[row] = 0;
+        if (uf & 8) *p_st = SIT_ST_NO_STEP;
+        if (uf & 4) *p_dn = 0;
         if (q >= 0 && q < a.io.request_capacity)
           for (int k = 0; k < SIT_OBS_DIM; ++k) a.io.request_obs[(size_t)q * SIT_OBS_DIM + k] = lo[k];
       } else {
@@ -371,20 +387,26 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       }
     }
     if (live) {
-      const T tn = xd.t[0][lane], te = xd.t[1][lane], on = xd.o[0][lane], oe = xd.o[1][lane];
+      // every LDS value of the step read up front (one wait; the empty asm keeps the reads out of
+      // the branches below)
+      T nt[6], no[4];
+      for (int q = 0; q < 6; ++q) nt[q] = xd.t[q][lane];
+      for (int q = 0; q < 4; ++q) no[q] = xd.o[q][lane];
+      const uint32_t bo = xd.bo[lane], f1 = xd.f[1][lane];
+      const T r_nto = xd.r_nto[lane], r_o = xd.r_o[lane];
+      asm volatile("" :: "v"(nt[0]), "v"(nt[1]), "v"(no[0]), "v"(no[1]), "v"(bo), "v"(f1), "v"(r_nto), "v"(r_o));
       const bool coll = coll_t;
-      const uint32_t bo = xd.bo[lane];
       env_done = (bits_t & SIT_ST_TEST_DONE) || (bo & kDoneBit) || coll;
-      const T dn = tn - on, de = te - oe;
-      const T r_snt = (bo & kStopBit) ? T(0) : (T(1) - xsqrt(dn * dn + de * de) * c.inv_maxn) * T(0.001);
+      const T dn = nt[0] - no[0], de = nt[1] - no[1];
+      const T snt = (T(1) - xsqrt(dn * dn + de * de) * c.inv_maxn) * T(0.001);
+      const T r_snt = (bo & kStopBit) ? T(0) : snt;
       const T rs = coll ? T(2000) : T(0);
-      const T reward = r_nt_t + r_term_t + xd.r_nto[lane] + xd.r_o[lane] + r_snt + rs;
+      const T reward = r_nt_t + r_term_t + r_nto + r_o + r_snt + rs;
       const uint32_t status = ((bits_t | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
-      const size_t row = (size_t)j * n_env + env;
-      if (uf & 2) a.io.reward[row] = reward;
-      if (uf & 4) a.io.done[row] = env_done ? 1 : 0;
-      if (uf & 8) a.io.status[row] = status;
-      const bool sac = (xd.f[1][lane] & kSfSac) != 0;
+      if (uf & 2) *p_rw = reward;
+      if (uf & 4) *p_dn = env_done ? 1 : 0;
+      if (uf & 8) *p_st = status;
+      const bool sac = (f1 & kSfSac) != 0;
       if (uf & kUfTrans) {             // replay transition of a sampling event (main_ast.py:385-396)
         const unsigned long long m = __ballot(sac);
         if (m) {
@@ -398,25 +420,22 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
             for (int q = 0; q < SIT_OBS_DIM; ++q) rec[q] = lo[q];
             rec[10] = xd.o[4][lane];
             rec[11] = reward;
-            for (int q = 0; q < 6; ++q) rec[12 + q] = xd.t[q][lane];
-            for (int q = 0; q < 4; ++q) rec[18 + q] = xd.o[q][lane];
+            for (int q = 0; q < 6; ++q) rec[12 + q] = nt[q];
+            for (int q = 0; q < 4; ++q) rec[18 + q] = no[q];
             const bool horizon_hit = (uf & kUfMaskH) && xd.ep[lane] + 2 == a.io.mask_horizon;
             rec[22] = (horizon_hit || !env_done) ? T(1) : T(0);
             rec[23] = (T)(a.io.env_id_offset + env);
           }
         }
       }
-      // (the LDS values read unconditionally, the initial observation in its own rare branch: a
-      // select between the two sources became generic-pointer loads)
-      for (int q = 0; q < 6; ++q) lo[q] = xd.t[q][lane];
-      for (int q = 0; q < 4; ++q) lo[6 + q] = xd.o[q][lane];
-      if (env_done)
-        for (int q = 0; q < SIT_OBS_DIM; ++q) lo[q] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + q];
+      for (int q = 0; q < 6; ++q) lo[q] = env_done ? li[q] : nt[q];
+      for (int q = 0; q < 4; ++q) lo[6 + q] = env_done ? li[6 + q] : no[q];
     }
     if (uf & kUfDoneCnt) {
       const unsigned long long m = __ballot(env_done);
-      if (lane == 0 && m) atomicAdd(a.io.done_count + j, (int)__popcll(m));
+      if (lane == 0 && m) atomicAdd(p_dc, (int)__popcll(m));
     }
+    p_rw += row_step; p_dn += row_step; p_st += row_step; ++p_dc;
   };
 
   SY_INIT();
