@@ -406,6 +406,24 @@ __device__ __forceinline__ void iw_point(double n, double e, double ab_len, doub
   iwe = e + ab_len * sin(ab_alpha + ang);
 }
 
+// the same IW in two parts: the direction (cos, sin)(AB_alpha + a), which depends only on the action
+// (the sync kernel draws the next event's action ahead, off its critical segment), and the point
+__device__ __forceinline__ void iw_dir(double ab_alpha, double ang, float& cs, float& sn) {
+  sincosf((float)(ab_alpha + ang), &sn, &cs);
+}
+__device__ __forceinline__ void iw_dir(double ab_alpha, double ang, double& cs, double& sn) {
+  cs = cos(ab_alpha + ang);
+  sn = sin(ab_alpha + ang);
+}
+__device__ __forceinline__ void iw_at(float n, float e, double ab_len, float cs, float sn, float& iwn, float& iwe) {
+  iwn = n + (float)ab_len * cs;
+  iwe = e + (float)ab_len * sn;
+}
+__device__ __forceinline__ void iw_at(double n, double e, double ab_len, double cs, double sn, double& iwn, double& iwe) {
+  iwn = n + ab_len * cs;
+  iwe = e + ab_len * sn;
+}
+
 // the sampler's seed made opaque where it is used: otherwise the compiler hoists Philox's ten-round
 // key schedule (18 uniform words) out of the step loop and spills it into VGPR lanes
 __device__ __forceinline__ uint64_t opaque_seed(uint64_t seed) {

@@ -35,14 +35,14 @@ constexpr int kSyncLanes = SIT_SYNC_LANES;
 
 // SIT_DIAG_SYNC (diagnostic builds only, tools/diag_sync.py): shader cycles per role and loop segment,
 // lane 0 of each wave, summed into g_sit_diag[role >> 1][(role & 1) * 8 + segment]: 0 work before
-// barrier A, 1 wait at A, 2 work A -> B, 3 wait at B, 4 work after B, 5 wave-steps, 6 P0's outputs
-// of the previous step (part of 2)
+// barrier A, 1 wait at A, 2 work A -> B, 3 wait at B, 4 work after B, 5 wave-steps, 6 and 7 P0's
+// outputs of the previous step up to the row stores / the rest (part of 2)
 #ifdef SIT_DIAG_SYNC
-#define SY_INIT() unsigned long long sy_t = __builtin_amdgcn_s_memtime(), sy_acc[7] = {0, 0, 0, 0, 0, 0, 0}
+#define SY_INIT() unsigned long long sy_t = __builtin_amdgcn_s_memtime(), sy_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define SY_MARK(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     sy_acc[k] += t_ - sy_t; sy_t = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
 #define SY_STEP() (sy_acc[5] += 1)
-#define SY_FLUSH(role) do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 7; ++q_) \
+#define SY_FLUSH(role) do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 8; ++q_) \
     atomicAdd(&g_sit_diag[(role) >> 1][((role) & 1) * 8 + q_], sy_acc[q_]); } while (0)
 #else
 #define SY_INIT() do { } while (0)
@@ -114,6 +114,12 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   // policy mode: the env's action slot (D1), and whether the env stopped for the policy
   bool ready = false, stalled = false;
   T pa = T(0);
+  // D1: the next sampling event's action and IW direction, drawn ahead (after the dynamics of the
+  // step that consumed the previous one, or in the prologue) so that the event itself, on the
+  // critical segment before barrier A, costs two multiply-adds
+  double nx_act = 0.0;
+  T nx_cs = T(0), nx_sn = T(0);
+  int32_t stall_q = -1;          // policy mode: the request slot whose noise is still to be drawn
   if (act) {
     ep_step = a.st.ep_step[env];
     load_ship(a.st, sid, s);
@@ -140,6 +146,14 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       }
     }
   }
+  // the next event's draw: mode-0 action U[-1, 1] (uniform_policy.py:20-22) from the sampler, or the
+  // policy's squashed action in [-1, 1]; the route angle is the action scaled by pi / 6
+  auto draw_next = [&]() {
+    nx_act = MODE == kPolicy ? (double)pa
+                             : sampler_uniform(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event) * 2.0 - 1.0;
+    iw_dir(ab_alpha, nx_act * (M_PI / 6.0), nx_cs, nx_sn);
+  };
+  if (TYPE == 1 && act && (MODE != kPolicy || ready)) draw_next();
   T p0[6] = {};
   int nw0 = 0;
   typename Route<T>::Leg leg0{};
@@ -171,24 +185,20 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         sac = ep_step == 0 || ((double)samp >= ab_len && !s.stop);
         int32_t q = kQLive;
         if (MODE == kPolicy && sac && !ready) {
-          // no action yet: the env waits for the policy; queue the request with this event's
-          // standard-normal draw (the reparameterised sample, normal.py:96-101)
+          // no action yet: the env waits for the policy; queue the request (its noise is drawn
+          // after barrier A)
           stalled = true;
           sac = false;
           q = atomicAdd(a.io.request_count, 1);
           if (q < a.io.request_capacity) {
             a.io.request_env[q] = env;
-            a.io.request_noise[q] = (T)sampler_normal(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
+            stall_q = q;
           }
-        } else if (sac) {
-          if (MODE == kPolicy) {          // the policy's squashed action in [-1, 1]
-            act_n = (double)pa;
-            ready = false;
-          } else {                        // mode-0 action U[-1, 1] (uniform_policy.py:20-22)
-            act_n = sampler_uniform(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event) * 2.0 - 1.0;
-          }
-          ang = act_n * (M_PI / 6.0);    // the route angle, scaled by the action bound pi / 6
-          iw_point(s.n, s.e, ab_len, ab_alpha, ang, iwn, iwe);
+        } else if (sac) {                 // the action drawn ahead (draw_next)
+          act_n = nx_act;
+          if (MODE == kPolicy) ready = false;
+          ang = act_n * (M_PI / 6.0);
+          iw_at(s.n, s.e, ab_len, nx_cs, nx_sn, iwn, iwe);
           ++event;
         }
         if (MODE == kPolicy) xd.q[lane] = q;
@@ -203,6 +213,11 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     __syncthreads();   // A: positions (and the IW, and in policy mode the step's decision) published
     SY_MARK(1);
     if (MODE == kPolicy && TYPE == 0 && act && !stalled) stalled = xd.q[lane] != kQLive;
+    if (MODE == kPolicy && TYPE == 1 && stall_q >= 0) {
+      // the request's standard-normal draw of this event (the reparameterised sample, normal.py:96-101)
+      a.io.request_noise[stall_q] = (T)sampler_normal(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
+      stall_q = -1;
+    }
     if (act && !stalled) {
       T o_rpm, o_ect, o_pme = T(0);
       bool ect_over = false;
@@ -243,6 +258,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         xd.o[4][lane] = (T)act_n;
         xd.f[1][lane] = fl;
         xd.ep[lane] = ep_step;
+        if (MODE != kPolicy && sac) draw_next();   // the next event's action (its counter is event)
       } else {
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
@@ -368,6 +384,7 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   uint32_t* p_st = (TYPE == 0 && (uf & 8)) ? a.io.status + env : nullptr;
   int* p_dc = (TYPE == 0 && (uf & kUfDoneCnt)) ? a.io.done_count : nullptr;
 
+  SY_INIT();
   // P0: reward, done, status, replay transition and done count of step j (MSRL_env_ex.py:906-980);
   // called once per step, in order
   auto outputs = [&](int j) {
@@ -406,6 +423,7 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       if (uf & 2) *p_rw = reward;
       if (uf & 4) *p_dn = env_done ? 1 : 0;
       if (uf & 8) *p_st = status;
+      SY_MARK(6);
       const bool sac = (f1 & kSfSac) != 0;
       if (uf & kUfTrans) {             // replay transition of a sampling event (main_ast.py:385-396)
         const unsigned long long m = __ballot(sac);
@@ -428,8 +446,12 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
           }
         }
       }
-      for (int q = 0; q < 6; ++q) lo[q] = env_done ? li[q] : nt[q];
-      for (int q = 0; q < 4; ++q) lo[6 + q] = env_done ? li[6 + q] : no[q];
+      // (the observation before the next step: every step when transitions or policy requests read
+      // it, else only at the last step, for last_obs)
+      if (MODE == kPolicy || (uf & kUfTrans) || j == n - 1) {
+        for (int q = 0; q < 6; ++q) lo[q] = env_done ? li[q] : nt[q];
+        for (int q = 0; q < 4; ++q) lo[6 + q] = env_done ? li[6 + q] : no[q];
+      }
     }
     if (uf & kUfDoneCnt) {
       const unsigned long long m = __ballot(env_done);
@@ -438,7 +460,6 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     p_rw += row_step; p_dn += row_step; p_st += row_step; ++p_dc;
   };
 
-  SY_INIT();
   for (int it = 0; it < n; ++it) {
     asm volatile("" : "+s"(uf));
     asm volatile("" : "+s"(map.use_index), "+s"(map.use_cells), "+s"(map.n_edge), "+s"(map.n_poly));
@@ -447,7 +468,7 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     __syncthreads();   // A: this step's positions
     SY_MARK(1);
     if (TYPE == 0 && it >= 1) outputs(it - 1);
-    SY_MARK(6);
+    SY_MARK(7);
     if (MODE == kPolicy && act && !stalled) stalled = xd.q[lane] != kQLive;
     // the predicates of the post-step position (MSRL_env_ex.py:460-603, 628-881): the map's (boundary
     // distance, hull in terrain, the IW test), arrival within 200 m of the final waypoint, the map

@@ -22,7 +22,7 @@ import torch  # noqa: E402
 from sac_maritime_ast_amd import VecMultiShipRLEnv, _lib, make_scenario  # noqa: E402
 
 SEGS = ["work before A", "wait A", "work A->B", "wait B", "work after B"]
-EXTRA = {6: "of which outputs of the previous step"}
+EXTRA = {6: "of which outputs up to the row stores", 7: "of which outputs after the stores"}
 ROLES = ["D0 test dynamics", "D1 obstacle dynamics", "P0 test predicates+outputs", "P1 obstacle predicates"]
 
 
@@ -59,14 +59,15 @@ def main():
     c = np.array(buf[:], dtype=np.float64).reshape(2, 32)
     out = {"kernel": env.lib.sit_step_kernel(env.handle).decode(), "roles": {}}
     for r, name in enumerate(ROLES):
-        row = c[r >> 1, (r & 1) * 8:(r & 1) * 8 + 7]
+        row = c[r >> 1, (r & 1) * 8:(r & 1) * 8 + 8]
         steps = max(row[5], 1.0)
-        # segment 6 (P0's outputs of the previous step) is stamped inside segment 2
+        # segments 6 and 7 (P0's outputs of the previous step) are stamped inside segment 2
         seg = row.copy()
-        seg[2] += seg[6]
+        seg[2] += seg[6] + seg[7]
         out["roles"][name] = {s_: round(seg[i] / steps, 1) for i, s_ in enumerate(SEGS)}
-        if seg[6]:
-            out["roles"][name][EXTRA[6]] = round(seg[6] / steps, 1)
+        for k in (6, 7):
+            if seg[k]:
+                out["roles"][name][EXTRA[k]] = round(seg[k] / steps, 1)
         out["roles"][name]["total"] = round(seg[:5].sum() / steps, 1)
     print(json.dumps(out, indent=1))
 
