@@ -130,6 +130,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     rt.tn = a.st.wn + (size_t)TYPE * a.cap * n_env + env;
     rt.te = a.st.we + (size_t)TYPE * a.cap * n_env + env;
     rt.stride = n_env;
+    rt.cap = a.cap;
     rt.load_leg(s.k);
     if (TYPE == 1) {
       samp = a.st.env[0][env]; eps = a.st.env[1][env];

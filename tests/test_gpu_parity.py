@@ -9,6 +9,9 @@ Contract:
     (per-field floors); discrete outputs identical except where the oracle's own decision
     margin lies inside the float32 band (counted and bounded).
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -25,6 +28,7 @@ from sac_maritime_ast_amd.config import params as sit_params  # noqa: E402
 from sac_maritime_ast_amd.scenario import Scenario  # noqa: E402
 
 DEV = "cuda:0"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TOL64 = 1e-9
 ENV_CASES = golden_names("env_")
 
@@ -480,42 +484,26 @@ def test_f32_synthetic_rollout_step_vs_oracle():
     assert n_sac > 0
 
 
-def test_f32_free_running_deviation_report():
-    """Reported, not gated: float32 vs float64 free-running from the same start, 4096
-    envs x 2000 steps of the synthetic sampler with auto-reset.  Per env the trajectories agree
-    until the first step whose discrete outputs differ (float32 state drift moving a decision);
-    printed: envs diverged, the earliest divergence, and the largest next_state deviation before it."""
-    n_env, steps, chunk = 4096, 2000, 500
-    sc = make_scenario(n_env, cap=48)
-    envs = [VecMultiShipRLEnv(scenario=sc, precision=p, device=DEV) for p in (32, 64)]
-    for e in envs:
-        e.reset()
-        e.init_step()
-    first = np.full(n_env, steps)
-    dev_max = np.zeros(n_env)
-    rew_max = np.zeros(n_env)
-    for k0 in range(0, steps, chunk):
-        o32, o64 = (e.rollout(chunk, seed=77) for e in envs)
-        d32, d64 = o32["done"].cpu().numpy(), o64["done"].cpu().numpy()
-        s32 = o32["status"].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
-        s64 = o64["status"].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
-        a32, a64 = o32["action"][..., 3].cpu().numpy(), o64["action"][..., 3].cpu().numpy()
-        e = rel_err(o32["next_state"].cpu().numpy(), o64["next_state"].cpu().numpy(), OBS_SCALE).max(-1)
-        # divergence: a discrete output differs, or the state jumps apart (> 1e-3: a waypoint switch
-        # or an episode event one step earlier or later)
-        diff = (d32 != d64) | (s32 != s64) | (a32 != a64) | (e > 1e-3)
-        step_idx = np.where(diff.any(0), diff.argmax(0) + k0, steps)
-        first = np.minimum(first, step_idx)
-        ok = (np.arange(k0, k0 + chunk)[:, None] < first[None, :])
-        dev_max = np.maximum(dev_max, np.where(ok, e, 0).max(0))
-        er = rel_err(o32["reward"].cpu().numpy(), o64["reward"].cpu().numpy(), 1.0)
-        rew_max = np.maximum(rew_max, np.where(ok, er, 0).max(0))
-    div = first < steps
-    print(f"f32 vs f64 free-running, {n_env} envs x {steps} steps: {int(div.sum())} envs diverged "
-          f"(earliest step {int(first.min()) if div.any() else None}, median {float(np.median(first[div])) if div.any() else None}); "
-          f"before divergence next_state rel dev max {dev_max.max():.2e}, p99 {np.percentile(dev_max, 99):.2e}, "
-          f"median {np.median(dev_max):.2e}; reward dev max {rew_max.max():.2e}")
-    assert np.isfinite(dev_max).all()
+def test_f32_free_running_within_storage_bound():
+    """float32 free-running against float64 from identical starts, 4096 envs x 2000
+    steps of the synthetic sampler with auto-reset, one step per launch (tools/f32_drift.py).  A third
+    run, the float64 kernel with its state rounded to float32 after every step, isolates what float32
+    state STORAGE alone costs.  Per env the runs are compared until the first step whose discrete
+    outcome differs (done, status, sampling event, waypoint index, route length, stop flags, episode
+    step, sampler counter).  Gated: before divergence the next_state deviation (per-field floors) is
+    within SURVEY §8(d)'s storage bound 2.5e-5; the float32 arithmetic adds at most 50 % to what
+    storage alone costs; at most 2 % of envs diverge (a decision moved by float32 state drift)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import f32_drift
+    rep = f32_drift.measure(4096, 2000, 77, log=False)
+    f32, s32 = rep["f32"], rep["s32"]
+    print(f"f32 vs f64 free-running: {f32['envs_diverged']} envs diverged (earliest step "
+          f"{f32['earliest_divergence_step']}), next_state max {f32['next_state_max']:.2e} p99 "
+          f"{f32['next_state_p99']:.2e}; float32 storage alone: {s32['envs_diverged']} diverged, max "
+          f"{s32['next_state_max']:.2e}")
+    assert f32["next_state_max"] <= 2.5e-5
+    assert f32["next_state_max"] <= 1.5 * s32["next_state_max"] + 1e-6
+    assert f32["envs_diverged"] <= 0.02 * 4096
 
 
 # ------------------------------------------------------------------------------------------

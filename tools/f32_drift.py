@@ -41,13 +41,9 @@ def rel(a, b, floor):
     return np.abs(a.astype(np.float64) - b.astype(np.float64)) / np.maximum(np.abs(b.astype(np.float64)), floor)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--n-env", type=int, default=4096)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--seed", type=int, default=77)
-    ap.add_argument("--out", default=None)
-    args = ap.parse_args()
+def measure(n_env=4096, steps=2000, seed=77, log=True):
+    """The report (a dict) of n_env envs x steps steps; tests/test_gpu_parity.py gates on it."""
+    args = argparse.Namespace(n_env=n_env, steps=steps, seed=seed)
     n = args.n_env
     sc = make_scenario(n, cap=48)
     envs = {k: VecMultiShipRLEnv(scenario=sc, precision=p, device="cuda:0") for k, p in (("f64", 64), ("f32", 32),
@@ -83,7 +79,7 @@ def main():
             for f in REAL:
                 e = rel(st[f], ref_s[f], SCALE[f])
                 st_dev[k][f] = np.where(ok[None, :], np.maximum(st_dev[k][f], e), st_dev[k][f])
-        if step % 200 == 0:
+        if log and step % 200 == 0:
             print(f"step {step}: diverged f32 {int((first['f32'] < args.steps).sum())}, "
                   f"s32 {int((first['s32'] < args.steps).sum())}", file=sys.stderr, flush=True)
     report = {"what": __doc__.split("\n\n")[0], "n_env": n, "steps": args.steps,
@@ -100,6 +96,17 @@ def main():
              "state_per_field_max": {f"{f}[{s}]": float(st_dev[k][f][s].max()) for f in REAL for s in (0, 1)},
              "argmax_env": int(ns_dev[k].max(1).argmax())}
         report[k] = r
+    return report
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-env", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--seed", type=int, default=77)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    report = measure(args.n_env, args.steps, args.seed)
     txt = json.dumps(report, indent=1)
     print(txt)
     if args.out:
