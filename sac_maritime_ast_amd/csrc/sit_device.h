@@ -749,6 +749,70 @@ __device__ __forceinline__ void ship_dynamics_pos(const Consts<T>& c, Ship<T>& s
   s.w = w + d_w * c.dt;
 }
 
+// ship_dynamics_pos in two parts with the same operations in the same order: DynBase holds every
+// term of the pre-step state alone (ship_model.py:596-603 without the rudder forces; the shaft
+// equation without the throttle; the thrust of the pre-step shaft speed), dyn_finish adds the rudder
+// and throttle terms and integrates.  The step kernel computes the base before guidance, so its
+// arithmetic fills the latency of guidance's serial chain.
+template <typename T>
+struct DynBase {
+  T ur;                 // surge relative to the current (the rudder forces' speed)
+  T f0, f1, f2;         // forces without the rudder terms
+  T inv_w;              // 1 / (w + 0.1) (the shaft equation's torque limit)
+};
+template <typename T, int MACH>
+__device__ __forceinline__ DynBase<T> dyn_base(const Consts<T>& c, const Ship<T>& s, T sp, T cp) {
+  const T u = s.u, v = s.v, r = s.r, w = s.w;
+  DynBase<T> b;
+  T thrust;
+  if (simpl_of<MACH>(c)) {
+    thrust = w;
+    b.inv_w = T(0);
+  } else {
+    b.inv_w = T(1) / (w + T(0.1));
+    thrust = c.thrust_k * w * xabs(w);
+  }
+  const T vc_u = cp * c.vc_n + sp * c.vc_e;
+  const T vc_v = -sp * c.vc_n + cp * c.vc_e;
+  const T ur = u - vc_u, vr = v - vc_v;
+  b.ur = ur;
+  const T uw = c.wind_speed * (c.wind_cos * cp + c.wind_sin * sp);
+  const T vw = c.wind_speed * (c.wind_sin * cp - c.wind_cos * sp);
+  const T urw = uw - u, vrw = vw - v;
+  const T wmag = xsqrt(urw * urw + vrw * vrw);
+  const T tau_u = c.wk_u * wmag * urw;
+  const T tau_v = c.wk_v * wmag * vrw;
+  const T tau_n = c.wk_n * urw * vrw;
+  const T mv = c.mass * v, mu = c.mass * u;
+  const T yv = c.y_dv * vr, xu = c.x_du * ur;
+  b.f0 = mv * r - yv * r - (c.d_u + c.ku * u) * ur + tau_u + thrust;
+  b.f1 = -mu * r + xu * r - (c.d_v + c.kv * v) * vr + tau_v;
+  b.f2 = -(mv * u - mu * v) - (-yv * ur + xu * vr) - (c.d_r + c.kr * r) * r + tau_n;
+  return b;
+}
+template <typename T, int MACH>
+__device__ __forceinline__ void dyn_finish(const Consts<T>& c, Ship<T>& s, const DynBase<T>& b, T thr, T rudder,
+                                           T n1, T e1) {
+  const T u = s.u, v = s.v, r = s.r, w = s.w;
+  T d_w;
+  if (simpl_of<MACH>(c)) {
+    d_w = (thr * c.p_simpl - c.k_thrust * w) * c.inv_tau;
+  } else {
+    const T tq_me = xmin(thr * c.avail_me * b.inv_w, c.tqcap_me);
+    const T tq_hsg = xmin(thr * c.avail_el * b.inv_w, c.tqcap_el);
+    d_w = ((tq_me - c.d_me * w) * c.inv_r_me + (tq_hsg - c.d_hsg * w) * c.inv_r_hsg - c.kp_prop * (w * w)) * c.inv_jp;
+  }
+  const T f_rv = -c.c_rv * rudder * b.ur;
+  const T f_rr = -c.c_rr * rudder * b.ur;
+  s.n = n1;
+  s.e = e1;
+  s.psi = s.psi + r * c.dt;
+  s.u = u + (c.inv_m11 * b.f0) * c.dt;
+  s.v = v + (c.inv_m22 * (b.f1 + f_rv)) * c.dt;
+  s.r = r + (c.inv_m33 * (b.f2 + f_rr)) * c.dt;
+  s.w = w + d_w * c.dt;
+}
+
 // --------------------------------------------------------------------------------------
 // polygon predicates (obstacle.py:126-141 -> GEOS)
 // --------------------------------------------------------------------------------------

@@ -34,16 +34,17 @@
 constexpr int kSyncLanes = SIT_SYNC_LANES;
 
 // SIT_DIAG_SYNC (diagnostic builds only, tools/diag_sync.py): shader cycles per role and loop segment,
-// lane 0 of each wave, summed into g_sit_diag[role >> 1][(role & 1) * 8 + segment]: 0 work before
-// barrier A, 1 wait at A, 2 work A -> B, 3 wait at B, 4 work after B, 5 wave-steps, 6 and 7 P0's
-// outputs of the previous step up to the row stores / the rest (part of 2)
+// lane 0 of each wave, summed into g_sit_diag[role >> 1][(role & 1) * 16 + segment]: 0 work before
+// barrier A, 1 wait at A, 2 work A -> B, 3 wait at B, 4 work after B, 5 wave-steps; 6 and 7 P0's
+// outputs of the previous step up to the row stores / the rest (part of 2); 8-11 sub-segments
+// (tools/diag_sync.py names them per role)
 #ifdef SIT_DIAG_SYNC
-#define SY_INIT() unsigned long long sy_t = __builtin_amdgcn_s_memtime(), sy_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define SY_INIT() unsigned long long sy_t = __builtin_amdgcn_s_memtime(), sy_acc[16] = {}
 #define SY_MARK(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     sy_acc[k] += t_ - sy_t; sy_t = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
 #define SY_STEP() (sy_acc[5] += 1)
-#define SY_FLUSH(role) do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 8; ++q_) \
-    atomicAdd(&g_sit_diag[(role) >> 1][((role) & 1) * 8 + q_], sy_acc[q_]); } while (0)
+#define SY_FLUSH(role) do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 16; ++q_) \
+    atomicAdd(&g_sit_diag[(role) >> 1][((role) & 1) * 16 + q_], sy_acc[q_]); } while (0)
 #else
 #define SY_INIT() do { } while (0)
 #define SY_MARK(k) do { } while (0)
@@ -168,18 +169,24 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   }
   uint32_t uf = __builtin_amdgcn_readfirstlane((c.collision_bias ? kUfCollBias : 0u) |
                                                (c.sg_mode != SIT_SG_MOTOR ? kUfBlackout : 0u));
+  // sine and cosine of the heading the next step starts from, taken where the heading is set (after
+  // the dynamics, which end before barrier B, where the D wave usually waits for the P wave; after an
+  // auto reset): the segment from B to A, on the step's critical path, then needs only the Euler
+  // position (its four multiply-adds) before publishing it
+  T sp_n = T(0), cp_n = T(1);
+  if (act) xsincos(s.psi, &sp_n, &cp_n);
 
   SY_INIT();
   for (int it = 0; it < n; ++it) {
     asm volatile("" : "+s"(uf));
     SyncSlot<T>& xd = X.d[it & 1];
-    T sp = T(0), cp = T(1);
+    const T sp = sp_n, cp = cp_n;
     T n1 = s.n, e1 = s.e;
     bool sac = false;
     double ang = 0.0, act_n = 0.0;
     if (act && !stalled) {
-      xsincos(s.psi, &sp, &cp);
       if (TYPE == 0 || !s.stop) euler_position(c, s, sp, cp, n1, e1);
+      SY_MARK(10);
       if (TYPE == 1) {
         // a sampling event: the episode's first step, or the sampling distance reaching AB_len while
         // the obstacle ship runs (test_beds/main_ast.py:337-349 with the SURVEY 8(d) converter)
@@ -236,12 +243,24 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
             samp = T(0);
           }
           const T pre_n = s.n, pre_e = s.e;
+          const DynBase<T> db = dyn_base<T, MACH>(c, s, sp, cp);   // independent of guidance: fills its latency
           T rudder, thr, psi_ref;
+#ifdef SIT_ABL_DG   // timing ablation (diagnostic builds only): no guidance / control
+          rudder = T(0); thr = T(0.5); o_ect = T(0); psi_ref = T(0);
+#else
           guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+#endif
+          SY_MARK(8);
           o_rpm = s.w * c.rpm_k;
           o_pme = power_me_kw(c, thr);
           s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
-          ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
+#ifdef SIT_ABL_DK   // timing ablation: no machinery / kinetics (the position still moves)
+          s.n = n1; s.e = e1; s.psi = s.psi + T(1e-3) * rudder;
+#else
+          dyn_finish<T, MACH>(c, s, db, thr, rudder, n1, e1);
+#endif
+          xsincos(s.psi, &sp_n, &cp_n);
+          SY_MARK(9);
           if (!init_f) {
             const T dn = pre_n - ppn, de = pre_e - ppe;
             const T d = xsqrt(dn * dn + de * de);
@@ -264,7 +283,13 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
         const T i1_0 = s.i1, i2_0 = s.i2;
+        const DynBase<T> db = dyn_base<T, MACH>(c, s, sp, cp);
+#ifdef SIT_ABL_DG
+        rudder = T(0); thr = T(0.5); o_ect = T(0); psi_ref = T(0);
+#else
         guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+#endif
+        SY_MARK(8);
         if (uf & kUfCollBias) {          // is_collision_imminent() on all-zero states (Q1)
           thr = xclip(thr * c.bias_scale, T(0), c.bias_max);
           rudder = xclip(rudder + c.bias_rudder, -c.rudder_max, c.rudder_max);
@@ -281,7 +306,13 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
                   > cs.x.blackout;
         }
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
-        ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
+#ifdef SIT_ABL_DK
+        s.n = n1; s.e = e1; s.psi = s.psi + T(1e-3) * rudder;
+#else
+        dyn_finish<T, MACH>(c, s, db, thr, rudder, n1, e1);
+#endif
+        xsincos(s.psi, &sp_n, &cp_n);
+        SY_MARK(9);
         s.ticks += 1;
         fl |= (mech ? kSfMech : 0u) | (ect_over ? kSfEct : 0u) | (blk ? kSfBlk : 0u);
         xd.t[0][lane] = s.n; xd.t[1][lane] = s.e; xd.t[2][lane] = s.psi;
@@ -303,6 +334,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       else if ((xd.f[1][lane] & kSfNav) || (pb1 & (kPbArrive | kPbHorizon | kPbIw)) || (pb0 & kPbColl)) s.stop = 1;
       rt.fixup(s.k);
       ep_step += 1;
+      SY_MARK(11);
       if (env_done) {
         // reset() (MSRL_Env.py:147-188; shaft speed and every PI/PID integrator persist, Q6) + init_step()
         s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];
@@ -312,6 +344,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         ep_step = 0;
         if (TYPE == 1) { samp = T(0); eps = T(0); ++episodes; }
         init_step_ship(c, cs.x, s, rt, v_des);
+        xsincos(s.psi, &sp_n, &cp_n);
       }
     }
     SY_MARK(4);
@@ -468,19 +501,29 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     SY_MARK(0);
     __syncthreads();   // A: this step's positions
     SY_MARK(1);
+#ifndef SIT_ABL_PO   // timing ablation: P0 writes no outputs
     if (TYPE == 0 && it >= 1) outputs(it - 1);
+#endif
     SY_MARK(7);
     if (MODE == kPolicy && act && !stalled) stalled = xd.q[lane] != kQLive;
     // the predicates of the post-step position (MSRL_env_ex.py:460-603, 628-881): the map's (boundary
     // distance, hull in terrain, the IW test), arrival within 200 m of the final waypoint, the map
     // horizon, and (P0) the ship-ship collision
+#ifdef SIT_ABL_PP   // timing ablation: no position predicates
+    if (act && !stalled) xd.pb[TYPE][lane] = 0u;
+    if (false) {
+#else
     if (act && !stalled) {
+#endif
       const T sn = xd.pn[TYPE][lane], se = xd.pe[TYPE][lane];
       DistPf<T> pf;
       pf_cell(c, map, sn, se, pf);
       pf_edges(map, pf);
+      SY_MARK(8);
       dobst = pf_finish(map, pf, sn, se);
+      SY_MARK(9);
       const bool terrain = hull_in_terrain_cls(c, map, sn, se, dobst, pf.cls, pf.cell_f, pf.word_f);
+      SY_MARK(10);
       pbits = (terrain ? kPbTerrain : 0u) | (within_radius(sn, se, end_n, end_e, c.arrive_d2_le) ? kPbArrive : 0u) |
               (outside(c, sn, se, c.half_len) ? kPbHorizon : 0u);
       if (TYPE == 1) {

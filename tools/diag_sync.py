@@ -22,7 +22,15 @@ import torch  # noqa: E402
 from sac_maritime_ast_amd import VecMultiShipRLEnv, _lib, make_scenario  # noqa: E402
 
 SEGS = ["work before A", "wait A", "work A->B", "wait B", "work after B"]
-EXTRA = {6: "of which outputs up to the row stores", 7: "of which outputs after the stores"}
+# sub-segments (part of the segment named first): D 10 = sincos + Euler position (before A), 8 = guidance
+# and control, 9 = machinery and kinetics (A->B), 11 = the episode-end decision (after B, the rest is the
+# reset); P 8 = cell record + first edge group issued, 9 = boundary distance, 10 = hull test (A->B);
+# P0 6 / 7 = the previous step's outputs up to the row stores / after them (A->B)
+SUB = {"D": {10: ("work before A", "sincos + Euler position"), 8: ("work A->B", "guidance + control"),
+             9: ("work A->B", "machinery + kinetics"), 11: ("work after B", "episode-end decision")},
+       "P": {6: ("work A->B", "P0 outputs up to the row stores"), 7: ("work A->B", "P0 outputs after the stores"),
+             8: ("work A->B", "cell record + first edges"), 9: ("work A->B", "boundary distance"),
+             10: ("work A->B", "hull test")}}
 ROLES = ["D0 test dynamics", "D1 obstacle dynamics", "P0 test predicates+outputs", "P1 obstacle predicates"]
 
 
@@ -59,16 +67,18 @@ def main():
     c = np.array(buf[:], dtype=np.float64).reshape(2, 32)
     out = {"kernel": env.lib.sit_step_kernel(env.handle).decode(), "roles": {}}
     for r, name in enumerate(ROLES):
-        row = c[r >> 1, (r & 1) * 8:(r & 1) * 8 + 8]
+        row = c[r >> 1, (r & 1) * 16:(r & 1) * 16 + 16]
         steps = max(row[5], 1.0)
-        # segments 6 and 7 (P0's outputs of the previous step) are stamped inside segment 2
-        seg = row.copy()
-        seg[2] += seg[6] + seg[7]
-        out["roles"][name] = {s_: round(seg[i] / steps, 1) for i, s_ in enumerate(SEGS)}
-        for k in (6, 7):
-            if seg[k]:
-                out["roles"][name][EXTRA[k]] = round(seg[k] / steps, 1)
-        out["roles"][name]["total"] = round(seg[:5].sum() / steps, 1)
+        sub = SUB[name[0]]
+        seg = {s_: row[i] for i, s_ in enumerate(SEGS)}
+        for k, (parent, _) in sub.items():      # a sub-segment's cycles belong to its parent segment
+            seg[parent] += row[k]
+        res = {s_: round(v / steps, 1) for s_, v in seg.items()}
+        for k, (parent, label) in sorted(sub.items()):
+            if row[k]:
+                res[f"  {parent}: {label}"] = round(row[k] / steps, 1)
+        res["total"] = round(sum(seg.values()) / steps, 1)
+        out["roles"][name] = res
     print(json.dumps(out, indent=1))
 
 
