@@ -222,8 +222,8 @@ struct Consts {
 
 // machinery model of a handle: a compile-time constant inside the step kernel (MACH = 0 shaft,
 // 1 simplified; k_env_steps dispatches once per wave), read from the constants elsewhere (-1)
-template <int MACH, typename T>
-__device__ __forceinline__ bool simpl_of(const Consts<T>& c) {
+template <int MACH, typename C>
+__device__ __forceinline__ bool simpl_of(const C& c) {
   if constexpr (MACH >= 0) return MACH == 1;
   else return c.mach_simpl != 0;
 }
@@ -480,8 +480,8 @@ __device__ SIT_LOS_EXACT_INLINE void los_exact(const ConstsX64& x, T n, T e, T p
 
 // ect_over: |e_ct| > e_tolerance (the navigation-failure predicate, MSRL_env_ex.py:560-576) decided
 // exactly (float64 inside the float32 band)
-template <typename T, int MACH = -1>
-__device__ __forceinline__ void guidance_control(const Consts<T>& c, const ConstsX64& x, Ship<T>& s, Route<T>& rt,
+template <typename T, int MACH = -1, typename C>
+__device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x, Ship<T>& s, Route<T>& rt,
                                                  T v_des, T& rudder, T& thr, T& ect_abs, T& psi_ref_out,
                                                  bool& ect_over) {
   // next_wpt: acceptance test evaluated in IEEE float64 from the stored values (the reference's
@@ -760,8 +760,8 @@ struct DynBase {
   T f0, f1, f2;         // forces without the rudder terms
   T inv_w;              // 1 / (w + 0.1) (the shaft equation's torque limit)
 };
-template <typename T, int MACH>
-__device__ __forceinline__ DynBase<T> dyn_base(const Consts<T>& c, const Ship<T>& s, T sp, T cp) {
+template <typename T, int MACH, typename C>
+__device__ __forceinline__ DynBase<T> dyn_base(const C& c, const Ship<T>& s, T sp, T cp) {
   const T u = s.u, v = s.v, r = s.r, w = s.w;
   DynBase<T> b;
   T thrust;
@@ -790,8 +790,8 @@ __device__ __forceinline__ DynBase<T> dyn_base(const Consts<T>& c, const Ship<T>
   b.f2 = -(mv * u - mu * v) - (-yv * ur + xu * vr) - (c.d_r + c.kr * r) * r + tau_n;
   return b;
 }
-template <typename T, int MACH>
-__device__ __forceinline__ void dyn_finish(const Consts<T>& c, Ship<T>& s, const DynBase<T>& b, T thr, T rudder,
+template <typename T, int MACH, typename C>
+__device__ __forceinline__ void dyn_finish(const C& c, Ship<T>& s, const DynBase<T>& b, T thr, T rudder,
                                            T n1, T e1) {
   const T u = s.u, v = s.v, r = s.r, w = s.w;
   T d_w;

@@ -1151,7 +1151,7 @@ struct sit_handle {
   int lds_attr[24] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
                       -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // dynamic-LDS size per step-kernel variant
   size_t map_bytes = 0;      // bytes staged into LDS: Edge[n_edge] + packed index
-  int lds_attr_sync[4] = {-1, -1, -1, -1};    // the same for k_env_steps_sync [mode policy][mach]
+  int lds_attr_sync[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // k_env_steps_sync [mode][mach][lds]
   // step-kernel selection, read once at sit_create (diagnostics / A-B runs only):
   //   SIT_STEP_KERNEL=classic  k_env_steps for every mode (default: k_env_steps_sync where it applies)
   //   SIT_LDS_MAP=0|1          map read through the caches / staged in LDS for every launch
@@ -1406,7 +1406,8 @@ template <typename T>
 void set_kernel_name(sit_handle* h, bool sync, int mode, bool lds, bool log, int mach) {
   static const char* const modes[3] = {"kExplicit", "kSynth", "kPolicy"};
   const char* t = kIsF32<T> ? "float" : "double";
-  if (sync) snprintf(h->last_kernel, sizeof(h->last_kernel), "k_env_steps_sync<%s,%s,MACH=%d>", t, modes[mode], mach);
+  if (sync) snprintf(h->last_kernel, sizeof(h->last_kernel), "k_env_steps_sync<%s,%s,%s,MACH=%d>", t, modes[mode],
+                     lds ? "map=LDS" : "map=global", mach);
   else snprintf(h->last_kernel, sizeof(h->last_kernel), "k_env_steps<%s,%s,%s,%s,MACH=%d>", t, modes[mode],
                 lds ? "map=LDS" : "map=global", log ? "log" : "nolog", mach);
 }
@@ -1418,31 +1419,39 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   const int mode = io.action_ne ? kExplicit : (io.policy_action ? kPolicy : kSynth);
   const int mach = a.c.mach_simpl ? 1 : 0;
   // k_env_steps_sync (sit_sync.h), two waves per ship with the map predicates on their own wave, for
-  // the rollouts with auto-reset whose actions come from the synthetic sampler (C3/C4: 1.75e10
-  // against 1.62e10 env-steps/s for k_env_steps) or from the policy (C5); k_env_steps for the
-  // explicit actions of sit_step, the trajectory log and rollouts without auto-reset
-  const size_t lds_sync = sync_lds_bytes<T>(h->map_bytes);
-  if (!h->kernel_classic && mode != kExplicit && !io.log && io.auto_reset && h->use_index &&
-      lds_sync + sizeof(Consts<T>) + 256 <= kLdsCu) {
-    const int slot = (mode == kPolicy ? 2 : 0) + mach;
-    const void* kern = mode == kPolicy ? (mach ? reinterpret_cast<const void*>(&k_env_steps_sync<T, kPolicy, 1>)
-                                               : reinterpret_cast<const void*>(&k_env_steps_sync<T, kPolicy, 0>))
-                                       : (mach ? reinterpret_cast<const void*>(&k_env_steps_sync<T, kSynth, 1>)
-                                               : reinterpret_cast<const void*>(&k_env_steps_sync<T, kSynth, 0>));
+  // every launch without the trajectory log: synthetic sampler (C3/C4), policy (C5) and explicit
+  // actions (sit_step, the drop-in MultiShipRLEnv.step).  k_env_steps (one wave per ship) runs the
+  // logged launches, and every launch under SIT_STEP_KERNEL=classic.  The sync kernel stages the map
+  // into LDS for fused launches; single-step launches read it through the caches.
+  const bool sync_lds = h->lds_map_sel == 1 || (h->lds_map_sel < 0 && io.n_steps >= kLdsMinSteps);
+  const size_t lds_sync = sync_lds ? sync_lds_bytes<T>(h->map_bytes) : sync_lds_bytes<T>(0);
+  if (!h->kernel_classic && !io.log && h->use_index && lds_sync + sizeof(Consts<T>) + 256 <= kLdsCu) {
+    const void* kern = nullptr;
+    auto pick = [&](auto mode_tag, auto mach_tag, auto lds_tag) {
+      constexpr int M = decltype(mode_tag)::value, K = decltype(mach_tag)::value;
+      constexpr bool L = decltype(lds_tag)::value;
+      kern = reinterpret_cast<const void*>(&k_env_steps_sync<T, M, K, L>);
+    };
+    auto pick_lds = [&](auto mode_tag, auto mach_tag) {
+      if (sync_lds) pick(mode_tag, mach_tag, std::true_type{});
+      else pick(mode_tag, mach_tag, std::false_type{});
+    };
+    auto pick_mach = [&](auto mode_tag) {
+      if (mach) pick_lds(mode_tag, std::integral_constant<int, 1>{});
+      else pick_lds(mode_tag, std::integral_constant<int, 0>{});
+    };
+    if (mode == kPolicy) pick_mach(std::integral_constant<int, kPolicy>{});
+    else if (mode == kSynth) pick_mach(std::integral_constant<int, kSynth>{});
+    else pick_mach(std::integral_constant<int, kExplicit>{});
+    const int slot = ((mode * 2 + mach) * 2) + (sync_lds ? 1 : 0);
     if (h->lds_attr_sync[slot] != (int)lds_sync) {
       HIP_TRY(h, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sync));
       h->lds_attr_sync[slot] = (int)lds_sync;
     }
     const int blocks = (h->n_env + kSyncLanes - 1) / kSyncLanes;
-    if (mode == kPolicy) {
-      if (mach) hipLaunchKernelGGL((k_env_steps_sync<T, kPolicy, 1>), dim3(blocks), dim3(256), lds_sync, stream, a);
-      else hipLaunchKernelGGL((k_env_steps_sync<T, kPolicy, 0>), dim3(blocks), dim3(256), lds_sync, stream, a);
-    } else {
-      if (mach) hipLaunchKernelGGL((k_env_steps_sync<T, kSynth, 1>), dim3(blocks), dim3(256), lds_sync, stream, a);
-      else hipLaunchKernelGGL((k_env_steps_sync<T, kSynth, 0>), dim3(blocks), dim3(256), lds_sync, stream, a);
-    }
-    HIP_TRY(h, hipGetLastError());
-    set_kernel_name<T>(h, true, mode, true, false, mach);
+    void* args[] = {&a};
+    HIP_TRY(h, hipLaunchKernel(kern, dim3(blocks), dim3(256), args, lds_sync, stream));
+    set_kernel_name<T>(h, true, mode, sync_lds, false, mach);
     return SIT_OK;
   }
   const int blocks = (h->n_env + kEnvsPerBlock * kGroups - 1) / (kEnvsPerBlock * kGroups);

@@ -100,6 +100,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
 #else
   const Consts<T> c = cs;
 #endif
+  // (a register copy of the guidance / control / dynamics constants measured 1.8 % slower at C3: 221
+  // instead of 174 VGPRs, more SGPR spills; the LDS reads are off the critical chain)
+  const Consts<T>& hc = cs;
   const int lane = threadIdx.x & (kWave - 1);
   const int n_env = a.n_env;
   const int sid = TYPE * n_env + env;
@@ -121,6 +124,17 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   double nx_act = 0.0;
   T nx_cs = T(0), nx_sn = T(0);
   int32_t stall_q = -1;          // policy mode: the request slot whose noise is still to be drawn
+  // explicit mode (D1): the caller's inputs of the next step, loaded one step ahead (the first step's
+  // with the prologue's loads), so no global load sits on the segment before barrier A
+  bool x_sac = false, x_init = false;
+  T x_an = T(0), x_ae = T(0);
+  auto load_inputs = [&](int step) {
+    const size_t row = (size_t)step * n_env + env;
+    x_sac = a.io.sac_update[row] != 0;
+    x_init = a.io.init[row] != 0;
+    x_an = a.io.action_ne[2 * row];
+    x_ae = a.io.action_ne[2 * row + 1];
+  };
   if (act) {
     ep_step = a.st.ep_step[env];
     load_ship(a.st, sid, s);
@@ -155,11 +169,13 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
                              : sampler_uniform(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event) * 2.0 - 1.0;
     iw_dir(ab_alpha, nx_act * (M_PI / 6.0), nx_cs, nx_sn);
   };
-  if (TYPE == 1 && act && (MODE != kPolicy || ready)) draw_next();
+  if (TYPE == 1 && act && (MODE == kSynth || (MODE == kPolicy && ready))) draw_next();
+  if (MODE == kExplicit && TYPE == 1 && act && n > 0) load_inputs(0);
   T p0[6] = {};
   int nw0 = 0;
   typename Route<T>::Leg leg0{};
-  if (act) {
+  const bool auto_reset = __builtin_amdgcn_readfirstlane(a.io.auto_reset) != 0;
+  if (act && auto_reset) {   // the episode start the auto reset restores (not loaded without it)
     for (int j = 0; j < 6; ++j) p0[j] = init_val(a.sc, TYPE, SIT_INIT_NORTH + j, env, n_env);
     nw0 = a.sc.nw0[sid];
     Route<T> r0 = rt;
@@ -168,7 +184,8 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     leg0 = r0.leg();
   }
   uint32_t uf = __builtin_amdgcn_readfirstlane((c.collision_bias ? kUfCollBias : 0u) |
-                                               (c.sg_mode != SIT_SG_MOTOR ? kUfBlackout : 0u));
+                                               (c.sg_mode != SIT_SG_MOTOR ? kUfBlackout : 0u) |
+                                               (auto_reset ? kUfAutoReset : 0u));
   // sine and cosine of the heading the next step starts from, taken where the heading is set (after
   // the dynamics, which end before barrier B, where the D wave usually waits for the P wave; after an
   // auto reset): the segment from B to A, on the step's critical path, then needs only the Euler
@@ -182,12 +199,21 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     SyncSlot<T>& xd = X.d[it & 1];
     const T sp = sp_n, cp = cp_n;
     T n1 = s.n, e1 = s.e;
-    bool sac = false;
+    bool sac = false, init_x = false;
     double ang = 0.0, act_n = 0.0;
     if (act && !stalled) {
       if (TYPE == 0 || !s.stop) euler_position(c, s, sp, cp, n1, e1);
       SY_MARK(10);
-      if (TYPE == 1) {
+      if (TYPE == 1 && MODE == kExplicit) {
+        // the caller's converted_action, SAC_update and init of this step (MultiShipRLEnv.step)
+        sac = x_sac;
+        init_x = x_init;
+        iwn = x_an;
+        iwe = x_ae;
+        if (it + 1 < n) load_inputs(it + 1);
+        xd.iwn[lane] = iwn; xd.iwe[lane] = iwe;
+        xd.ang[lane] = angle_or_nan(false, T(0));   // no device draw
+      } else if (TYPE == 1) {
         // a sampling event: the episode's first step, or the sampling distance reaching AB_len while
         // the obstacle ship runs (test_beds/main_ast.py:337-349 with the SURVEY 8(d) converter)
         sac = ep_step == 0 || ((double)samp >= ab_len && !s.stop);
@@ -231,7 +257,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       bool ect_over = false;
       uint32_t fl = s.stop ? kSfStopPre : 0u;
       if (TYPE == 1) {
-        const bool init_f = ep_step == 0;
+        const bool init_f = MODE == kExplicit ? init_x : ep_step == 0;
         if (sac) fl |= kSfSac;
         if (s.stop) {                    // obs_step (MSRL_Env.py:287-402): stop path (Q10)
           s.ticks += 2;
@@ -243,12 +269,12 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
             samp = T(0);
           }
           const T pre_n = s.n, pre_e = s.e;
-          const DynBase<T> db = dyn_base<T, MACH>(c, s, sp, cp);   // independent of guidance: fills its latency
+          const DynBase<T> db = dyn_base<T, MACH>(hc, s, sp, cp);   // independent of guidance: fills its latency
           T rudder, thr, psi_ref;
 #ifdef SIT_ABL_DG   // timing ablation (diagnostic builds only): no guidance / control
           rudder = T(0); thr = T(0.5); o_ect = T(0); psi_ref = T(0);
 #else
-          guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+          guidance_control<T, MACH>(hc, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
 #endif
           SY_MARK(8);
           o_rpm = s.w * c.rpm_k;
@@ -257,7 +283,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
 #ifdef SIT_ABL_DK   // timing ablation: no machinery / kinetics (the position still moves)
           s.n = n1; s.e = e1; s.psi = s.psi + T(1e-3) * rudder;
 #else
-          dyn_finish<T, MACH>(c, s, db, thr, rudder, n1, e1);
+          dyn_finish<T, MACH>(hc, s, db, thr, rudder, n1, e1);
 #endif
           xsincos(s.psi, &sp_n, &cp_n);
           SY_MARK(9);
@@ -275,19 +301,19 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         const bool nav = ect_over || (double)samp > samp_limit;
         fl |= nav ? kSfNav : 0u;
         xd.o[0][lane] = s.n; xd.o[1][lane] = s.e; xd.o[2][lane] = s.psi; xd.o[3][lane] = o_ect;
-        xd.o[4][lane] = (T)act_n;
+        xd.o[4][lane] = MODE == kExplicit ? angle_or_nan(false, T(0)) : (T)act_n;
         xd.f[1][lane] = fl;
         xd.ep[lane] = ep_step;
-        if (MODE != kPolicy && sac) draw_next();   // the next event's action (its counter is event)
+        if (MODE == kSynth && sac) draw_next();   // the next event's action (its counter is event)
       } else {
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
         const T i1_0 = s.i1, i2_0 = s.i2;
-        const DynBase<T> db = dyn_base<T, MACH>(c, s, sp, cp);
+        const DynBase<T> db = dyn_base<T, MACH>(hc, s, sp, cp);
 #ifdef SIT_ABL_DG
         rudder = T(0); thr = T(0.5); o_ect = T(0); psi_ref = T(0);
 #else
-        guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
+        guidance_control<T, MACH>(hc, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
 #endif
         SY_MARK(8);
         if (uf & kUfCollBias) {          // is_collision_imminent() on all-zero states (Q1)
@@ -309,7 +335,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
 #ifdef SIT_ABL_DK
         s.n = n1; s.e = e1; s.psi = s.psi + T(1e-3) * rudder;
 #else
-        dyn_finish<T, MACH>(c, s, db, thr, rudder, n1, e1);
+        dyn_finish<T, MACH>(hc, s, db, thr, rudder, n1, e1);
 #endif
         xsincos(s.psi, &sp_n, &cp_n);
         SY_MARK(9);
@@ -335,7 +361,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       rt.fixup(s.k);
       ep_step += 1;
       SY_MARK(11);
-      if (env_done) {
+      if ((uf & kUfAutoReset) && env_done) {
         // reset() (MSRL_Env.py:147-188; shaft speed and every PI/PID integrator persist, Q6) + init_step()
         s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];
         s.ect_int = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
@@ -373,22 +399,26 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
 template <typename T, int MODE, int TYPE>
 __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, const Map<T>& map_in,
                                       SyncShared<T>& X, int env, bool act) {
-  const Consts<T> c = cs;
+  const Consts<T> c = cs;   // a register copy (reading the LDS copy where used measured 11 % slower)
   Map<T> map = map_in;
   const int lane = threadIdx.x & (kWave - 1);
   const int n_env = a.n_env;
   const int n = a.io.n_steps;
-  T iw_tn = T(0), iw_te = T(0);     // P1: the IW test's cache (the IW changes at sampling events)
+  // P1: the IW test's cache (the IW changes at sampling events).  (Carrying it across launches in the
+  // state saved single-step launches 0.2 us and cost C3 1.4 %: a load, a store and three more SGPR
+  // spills on the P waves.)
+  T iw_tn = T(0), iw_te = T(0);
   bool iw_valid = false, iw_in = false;
   T lo[SIT_OBS_DIM] = {};           // P0: the observation before the step (replay transition)
   // P0: the episode's initial observation, held in registers: a load of it inside the loop left a
   // global load pending on lo's registers, and the next step's LDS reads into them waited for every
   // outstanding memory operation (s_waitcnt vmcnt(0)), the step's output stores included (~1 000 cycles)
   T li[SIT_OBS_DIM] = {};
+  const bool auto_reset = __builtin_amdgcn_readfirstlane(a.io.auto_reset) != 0;
   if (TYPE == 0 && act)
     for (int j = 0; j < SIT_OBS_DIM; ++j) {
       lo[j] = a.st.last_obs[(size_t)j * n_env + env];
-      li[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
+      if (auto_reset) li[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
     }
   // (drained here, so that no load is pending on li's registers when the loop first reads them)
   __builtin_amdgcn_s_waitcnt(0);
@@ -405,7 +435,8 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
                                                (a.io.done ? 4u : 0u) | (a.io.status ? 8u : 0u) |
                                                (a.io.action_out ? 16u : 0u) | (a.io.transitions ? kUfTrans : 0u) |
                                                (a.io.done_count ? kUfDoneCnt : 0u) |
-                                               (a.io.mask_horizon > 0 ? kUfMaskH : 0u));
+                                               (a.io.mask_horizon > 0 ? kUfMaskH : 0u) |
+                                               (auto_reset ? kUfAutoReset : 0u));
   // this ship's next_state columns (P0: 0-5, P1: 6-9) and, P1, the IW action row, one row block per step
   T* p_ns = (uf & 1) ? a.io.next_state + (size_t)env * SIT_OBS_DIM + (TYPE == 0 ? 0 : 6) : nullptr;
   T* p_ao = (TYPE == 1 && (uf & 16)) ? a.io.action_out + (size_t)env * 4 : nullptr;
@@ -483,8 +514,9 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       // (the observation before the next step: every step when transitions or policy requests read
       // it, else only at the last step, for last_obs)
       if (MODE == kPolicy || (uf & kUfTrans) || j == n - 1) {
-        for (int q = 0; q < 6; ++q) lo[q] = env_done ? li[q] : nt[q];
-        for (int q = 0; q < 4; ++q) lo[6 + q] = env_done ? li[6 + q] : no[q];
+        const bool restart = (uf & kUfAutoReset) && env_done;   // the auto reset's initial observation
+        for (int q = 0; q < 6; ++q) lo[q] = restart ? li[q] : nt[q];
+        for (int q = 0; q < 4; ++q) lo[6 + q] = restart ? li[6 + q] : no[q];
       }
     }
     if (uf & kUfDoneCnt) {
@@ -508,7 +540,8 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     if (MODE == kPolicy && act && !stalled) stalled = xd.q[lane] != kQLive;
     // the predicates of the post-step position (MSRL_env_ex.py:460-603, 628-881): the map's (boundary
     // distance, hull in terrain, the IW test), arrival within 200 m of the final waypoint, the map
-    // horizon, and (P0) the ship-ship collision
+    // horizon, and (P0) the ship-ship collision.  (Reading the cell record and first edges before
+    // P0's outputs, to overlap their latency, measured 3 % slower.)
 #ifdef SIT_ABL_PP   // timing ablation: no position predicates
     if (act && !stalled) xd.pb[TYPE][lane] = 0u;
     if (false) {
@@ -622,19 +655,21 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   }
 }
 
-template <typename T, int MODE, int MACH>
+// LDSMAP: the island map staged into LDS per block (fused launches) or read through the caches
+// (single-step launches, whose prologue cannot amortise staging 57 KB per block)
+template <typename T, int MODE, int MACH, bool LDSMAP>
 __global__ __launch_bounds__(256) void k_env_steps_sync(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Consts<T> cs;
   for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
     reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
-  const Map<T> map = stage_map(a, smem);
+  const Map<T> map = LDSMAP ? stage_map(a, smem) : a.map;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int role = (blockIdx.x & 1) == 0 ? w : (w ^ 2);
   const int lane = threadIdx.x & (kWave - 1);
   const int env = blockIdx.x * kSyncLanes + lane;
   const bool act = lane < kSyncLanes && env < a.n_env;
-  SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(smem + (((size_t)a.map_bytes + 255) & ~size_t(255)));
+  SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(smem + (LDSMAP ? (((size_t)a.map_bytes + 255) & ~size_t(255)) : 0));
   __syncthreads();   // constants copied, map staged
   if (role == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, env, act);
   else if (role == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, env, act);

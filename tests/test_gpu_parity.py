@@ -717,3 +717,35 @@ def test_c4_last_shard_full_size():
     o = small.rollout(200, seed=25450, env_id_offset=off)
     for k in head:
         assert np.array_equal(o[k].cpu().numpy(), head[k]), k
+
+
+@pytest.mark.parametrize("kernel", ["sync", "classic"])
+@pytest.mark.parametrize("precision", [64, 32])
+def test_launch_partition_invariance(precision, kernel, monkeypatch):
+    """One 300-step launch equals 300 one-step launches bit for bit (synthetic sampler, auto-reset):
+    everything a launch keeps in registers across steps (the route leg cache, the sampler's next draw,
+    the next heading's sine and cosine, the IW test's cache) is rebuilt from the state at the next
+    launch with the same values.  With the one-wave kernel the one-step launches also read the map
+    through the caches instead of LDS."""
+    if kernel == "classic":
+        monkeypatch.setenv("SIT_STEP_KERNEL", "classic")
+    n_env, steps = 512, 300
+    outs = []
+    for k in (steps, 1):
+        env = VecMultiShipRLEnv(scenario=make_scenario(n_env, cap=48), precision=precision, device=DEV)
+        env.reset()
+        env.init_step()
+        rows = {q: [] for q in ("next_state", "reward", "done", "status", "action")}
+        for _ in range(steps // k):
+            o = env.rollout(k, seed=13, transition_capacity=0)
+            for q in rows:
+                rows[q].append(o[q].cpu().numpy())
+        outs.append(({q: np.concatenate(v) for q, v in rows.items()}, np_state(env), env))
+    (a, sa, ea), (b, sb, eb) = outs
+    assert ea.lib.sit_step_kernel(ea.handle).decode().startswith("k_env_steps_sync" if kernel == "sync" else "k_env_steps<")
+    for q in a:
+        assert np.array_equal(a[q], b[q], equal_nan=True), q
+    for q in sa:
+        assert np.array_equal(sa[q], sb[q]), q
+    iw = int(((a["status"] & _lib.ST_OBS_IW_TERMINAL) != 0).sum())
+    print(f"launch partition f{precision} {kernel}: {iw} IW terminations, identical")
