@@ -68,12 +68,18 @@ const FieldSpec kFields[] = {
     // trajectory log only: accumulated fuel per ship, the obstacle ship's last logged row
     {"fuel_me", SIT_DT_REAL, kShip},      {"fuel_el", SIT_DT_REAL, kShip},
     {"fuel", SIT_DT_REAL, kShip},         {"last_log", SIT_DT_REAL, kLogRow},
+    // the IW terrain test's last result, keyed by the point it was taken at (obstacle.py's
+    // Polygon.contains of a fixed map is a function of the point): single-step launches, which
+    // cannot keep it in registers across steps, reuse it while the caller's IW does not change.
+    // iw_key_flags bit 0 = valid, bit 1 = inside; sit_load_map clears it
+    {"iw_key_north", SIT_DT_REAL, kEnv},  {"iw_key_east", SIT_DT_REAL, kEnv},
+    {"iw_key_flags", SIT_DT_U32, kEnv},
 };
 constexpr int kNumFields = (int)(sizeof(kFields) / sizeof(kFields[0]));
 enum FieldId {
   F_NORTH = 0, F_LAST_PME = 14, F_K = 15, F_NW, F_TICKS, F_STOP,
   F_SAMP = 19, F_IW_E = 24, F_EP = 25, F_EVENT, F_EPISODES, F_WN, F_WE, F_LAST_OBS,
-  F_FUEL_ME, F_FUEL_EL, F_FUEL, F_LAST_LOG
+  F_FUEL_ME, F_FUEL_EL, F_FUEL, F_LAST_LOG, F_IWK_N, F_IWK_E, F_IWK_FLAGS
 };
 
 // per-env scenario (constant after sit_load_*), device side
@@ -104,7 +110,10 @@ struct State {
   T* last_obs;            // [SIT_OBS_DIM][n_env]: observation before the next step
   T* fuel[3];             // [2 * n_env] each: fuel me, fuel electrical, fuel total (log only)
   T* last_log;            // [SIT_LOG_KEYS][n_env]: the obstacle's last logged row (log only)
+  T* iwk[2];              // [n_env] each: the point of the cached IW test
+  uint32_t* iwk_flags;    // [n_env]: kIwkValid | kIwkInside
 };
+constexpr uint32_t kIwkValid = 1u, kIwkInside = 2u;
 
 template <typename T>
 struct StepIO {
@@ -1355,6 +1364,8 @@ KArgs<T> make_args(const sit_handle* h) {
   a.st.last_obs = fp(F_LAST_OBS);
   for (int i = 0; i < 3; ++i) a.st.fuel[i] = fp(F_FUEL_ME + i);
   a.st.last_log = fp(F_LAST_LOG);
+  a.st.iwk[0] = fp(F_IWK_N); a.st.iwk[1] = fp(F_IWK_E);
+  a.st.iwk_flags = reinterpret_cast<uint32_t*>(h->blob + h->off[F_IWK_FLAGS]);
   a.sc.init = reinterpret_cast<const T*>(h->scen + h->scen_init);
   a.sc.end_n = reinterpret_cast<const T*>(h->scen + h->scen_end_n);
   a.sc.end_e = reinterpret_cast<const T*>(h->scen + h->scen_end_e);

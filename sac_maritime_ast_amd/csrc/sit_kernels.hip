@@ -549,6 +549,8 @@ int sit_load_map(sit_handle* h, int32_t n_poly, const int32_t* vert_offsets, con
   h->n_poly = n_poly;
   h->n_vert = nv;
   h->have_map = true;
+  // the cached IW tests describe the previous map
+  HIP_TRY(h, setup_zero(h->blob + h->off[F_IWK_FLAGS], (size_t)h->n_env * 4));
   return SIT_OK;
 }
 

@@ -107,6 +107,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   const int n_env = a.n_env;
   const int sid = TYPE * n_env + env;
   const int n = a.io.n_steps;
+  SY_INIT();
 
   Ship<T> s{};
   Route<T> rt{};
@@ -193,7 +194,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   T sp_n = T(0), cp_n = T(1);
   if (act) xsincos(s.psi, &sp_n, &cp_n);
 
-  SY_INIT();
+  SY_MARK(12);   // prologue
   for (int it = 0; it < n; ++it) {
     asm volatile("" : "+s"(uf));
     SyncSlot<T>& xd = X.d[it & 1];
@@ -376,7 +377,6 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     SY_MARK(4);
     SY_STEP();
   }
-  SY_FLUSH(TYPE);
   __syncthreads();   // C: P1's reward terms of the last step (P0 writes that step's outputs)
   if (act) {
     store_ship(a.st, sid, s);
@@ -391,12 +391,14 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       if (MODE == kPolicy) a.io.policy_ready[env] = ready ? 1 : 0;
     }
   }
+  SY_MARK(13);   // epilogue (the wait at barrier C, the state write-back)
+  SY_FLUSH(TYPE);
 }
 
 // ------------------------------------------------------------------------------------------
 // P waves
 // ------------------------------------------------------------------------------------------
-template <typename T, int MODE, int TYPE>
+template <typename T, int MODE, int TYPE, bool LDSMAP>
 __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, const Map<T>& map_in,
                                       SyncShared<T>& X, int env, bool act) {
   const Consts<T> c = cs;   // a register copy (reading the LDS copy where used measured 11 % slower)
@@ -404,11 +406,20 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   const int lane = threadIdx.x & (kWave - 1);
   const int n_env = a.n_env;
   const int n = a.io.n_steps;
-  // P1: the IW test's cache (the IW changes at sampling events).  (Carrying it across launches in the
-  // state saved single-step launches 0.2 us and cost C3 1.4 %: a load, a store and three more SGPR
-  // spills on the P waves.)
+  SY_INIT();
+  // P1: the IW test's cache (the IW changes at sampling events).  Single-step launches (the map read
+  // through the caches, LDSMAP false) carry it across launches in the state (iw_key_*): there the
+  // test's chain of dependent map reads is the step's longest path, and the drop-in's caller passes
+  // the same IW until its next sampling event.  (Fused launches keep it in registers only: carrying
+  // it cost C3 1.4 %, a load, a store and three more SGPR spills.)
   T iw_tn = T(0), iw_te = T(0);
   bool iw_valid = false, iw_in = false;
+  if (!LDSMAP && TYPE == 1 && act) {
+    const uint32_t f = a.st.iwk_flags[env];
+    iw_tn = a.st.iwk[0][env]; iw_te = a.st.iwk[1][env];
+    iw_valid = (f & kIwkValid) != 0;
+    iw_in = (f & kIwkInside) != 0;
+  }
   T lo[SIT_OBS_DIM] = {};           // P0: the observation before the step (replay transition)
   // P0: the episode's initial observation, held in registers: a load of it inside the loop left a
   // global load pending on lo's registers, and the next step's LDS reads into them waited for every
@@ -449,7 +460,7 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   uint32_t* p_st = (TYPE == 0 && (uf & 8)) ? a.io.status + env : nullptr;
   int* p_dc = (TYPE == 0 && (uf & kUfDoneCnt)) ? a.io.done_count : nullptr;
 
-  SY_INIT();
+  SY_MARK(12);   // prologue
   // P0: reward, done, status, replay transition and done count of step j (MSRL_env_ex.py:906-980);
   // called once per step, in order
   auto outputs = [&](int j) {
@@ -641,7 +652,6 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     SY_MARK(4);
     SY_STEP();
   }
-  SY_FLUSH(2 + TYPE);
   __syncthreads();   // C
   if (TYPE == 0) {
     if (n >= 1) outputs(n - 1);
@@ -653,6 +663,12 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       if (lane == 0 && v) atomicAdd(a.io.env_steps, v);
     }
   }
+  if (!LDSMAP && TYPE == 1 && act) {
+    a.st.iwk[0][env] = iw_tn; a.st.iwk[1][env] = iw_te;
+    a.st.iwk_flags[env] = iw_valid ? (kIwkValid | (iw_in ? kIwkInside : 0u)) : 0u;
+  }
+  SY_MARK(13);   // epilogue (the wait at barrier C, P0's last outputs and last_obs)
+  SY_FLUSH(2 + TYPE);
 }
 
 // LDSMAP: the island map staged into LDS per block (fused launches) or read through the caches
@@ -673,6 +689,6 @@ __global__ __launch_bounds__(256) void k_env_steps_sync(const KArgs<T> a) {
   __syncthreads();   // constants copied, map staged
   if (role == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, env, act);
   else if (role == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, env, act);
-  else if (role == 2) sync_p<T, MODE, 0>(a, cs, map, X, env, act);
-  else sync_p<T, MODE, 1>(a, cs, map, X, env, act);
+  else if (role == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, env, act);
+  else sync_p<T, MODE, 1, LDSMAP>(a, cs, map, X, env, act);
 }

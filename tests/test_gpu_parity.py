@@ -724,9 +724,9 @@ def test_c4_last_shard_full_size():
 def test_launch_partition_invariance(precision, kernel, monkeypatch):
     """One 300-step launch equals 300 one-step launches bit for bit (synthetic sampler, auto-reset):
     everything a launch keeps in registers across steps (the route leg cache, the sampler's next draw,
-    the next heading's sine and cosine, the IW test's cache) is rebuilt from the state at the next
-    launch with the same values.  With the one-wave kernel the one-step launches also read the map
-    through the caches instead of LDS."""
+    the next heading's sine and cosine) is rebuilt from the state at the next launch with the same
+    values, and the one-step launches' IW-test cache (iw_key_*, keyed by the IW point) returns what the
+    test would.  The one-step launches read the map through the caches instead of LDS."""
     if kernel == "classic":
         monkeypatch.setenv("SIT_STEP_KERNEL", "classic")
     n_env, steps = 512, 300
@@ -746,6 +746,7 @@ def test_launch_partition_invariance(precision, kernel, monkeypatch):
     for q in a:
         assert np.array_equal(a[q], b[q], equal_nan=True), q
     for q in sa:
-        assert np.array_equal(sa[q], sb[q]), q
+        if not q.startswith("iw_key"):   # the single-step launches' IW-test cache (not model state)
+            assert np.array_equal(sa[q], sb[q]), q
     iw = int(((a["status"] & _lib.ST_OBS_IW_TERMINAL) != 0).sum())
     print(f"launch partition f{precision} {kernel}: {iw} IW terminations, identical")

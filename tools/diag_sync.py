@@ -26,11 +26,13 @@ SEGS = ["work before A", "wait A", "work A->B", "wait B", "work after B"]
 # and control, 9 = machinery and kinetics (A->B), 11 = the episode-end decision (after B, the rest is the
 # reset); P 8 = cell record + first edge group issued, 9 = boundary distance, 10 = hull test (A->B);
 # P0 6 / 7 = the previous step's outputs up to the row stores / after them (A->B)
-SUB = {"D": {10: ("work before A", "sincos + Euler position"), 8: ("work A->B", "guidance + control"),
-             9: ("work A->B", "machinery + kinetics"), 11: ("work after B", "episode-end decision")},
+SUB = {"D": {10: ("work before A", "Euler position"), 8: ("work A->B", "dynamics base + guidance + control"),
+             9: ("work A->B", "machinery + kinetics + next heading trig"),
+             11: ("work after B", "episode-end decision")},
        "P": {6: ("work A->B", "P0 outputs up to the row stores"), 7: ("work A->B", "P0 outputs after the stores"),
              8: ("work A->B", "cell record + first edges"), 9: ("work A->B", "boundary distance"),
              10: ("work A->B", "hull test")}}
+ONCE = {12: "prologue (per launch)", 13: "epilogue (per launch)"}
 ROLES = ["D0 test dynamics", "D1 obstacle dynamics", "P0 test predicates+outputs", "P1 obstacle predicates"]
 
 
@@ -40,6 +42,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=2000)
     ap.add_argument("--launches", type=int, default=5)
     ap.add_argument("--policy", action="store_true")
+    ap.add_argument("--step", action="store_true", help="explicit actions, one launch per step (sit_step)")
     args = ap.parse_args()
     lib = ctypes.CDLL(_lib.LIB_PATH)
     lib.sit_diag_read_f32.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
@@ -47,7 +50,18 @@ def main():
     env = VecMultiShipRLEnv(scenario=make_scenario(args.n_env, cap=48), precision=32, device="cuda:0")
     env.reset()
     env.init_step()
-    if args.policy:
+    if args.step:
+        g = torch.Generator(device="cuda:0").manual_seed(1)
+        st = env.get_state()
+        act = torch.stack([st["north"][1], st["east"][1]], 1) + torch.randn(args.n_env, 2, device="cuda:0", generator=g) * 500
+        sac = (torch.rand(args.n_env, device="cuda:0", generator=g) < 0.005).to(torch.uint8)
+        init = torch.zeros(args.n_env, dtype=torch.uint8, device="cuda:0")
+
+        def run():
+            env.step(act, sac, init)
+        for _ in range(200):
+            run()
+    elif args.policy:
         from sac_maritime_ast_amd.samplers import GaussianPolicy, PolicySampler
         torch.manual_seed(0)
         sm = PolicySampler(env, GaussianPolicy().to("cuda:0"), chunk=64, request_capacity=args.n_env // 4)
@@ -60,7 +74,7 @@ def main():
         for _ in range(max(1, 40000 // args.chunk)):
             run()
     assert lib.sit_diag_read_f32(buf, 1) == 0
-    for _ in range(args.launches if not args.policy else 200):
+    for _ in range(args.launches if not (args.policy or args.step) else 200):
         run()
     torch.cuda.synchronize()
     assert lib.sit_diag_read_f32(buf, 0) == 0
@@ -78,6 +92,10 @@ def main():
             if row[k]:
                 res[f"  {parent}: {label}"] = round(row[k] / steps, 1)
         res["total"] = round(sum(seg.values()) / steps, 1)
+        launches = max(1, args.launches if not (args.policy or args.step) else 200)
+        waves = launches * ((args.n_env + 63) // 64)
+        for k, label in ONCE.items():   # per wave and launch
+            res[label] = round(row[k] / waves, 1)
         out["roles"][name] = res
     print(json.dumps(out, indent=1))
 
