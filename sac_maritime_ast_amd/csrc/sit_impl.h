@@ -297,7 +297,7 @@ __device__ __forceinline__ double angle_or_nan(bool has, double a) {
 //           sampling event without a fresh action waits for the rest of the launch and queues
 //           a request; the next launch consumes the action the policy wrote for it)
 // ---------------------------------------------------------------------------------------
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC)
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC) || defined(SIT_DIAG_PLACE)
 // Diagnostic builds only (tools/diag_paths.py, tools/diag_sync.py): [type][0..15] predicate path
 // statistics, [type][16..23] shader-clock cycles per step phase (wave lane 0); SIT_DIAG_SYNC: cycles
 // per role and segment of k_env_steps_sync (sit_sync.h).  The counters are per translation unit:
@@ -314,10 +314,17 @@ int diag_read_impl(unsigned long long* out, int reset) {
   return 0;
 }
 #endif
-#ifdef SIT_DIAG_PHASES
+#if defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_PLACE)
 // per wave of the last launch: start / end (realtime ticks), shader cycles, HW_ID | XCC_ID << 32
+// (SIT_DIAG_PLACE, the two-wave kernel, tools/diag_place.py: role, block, -, HW_ID | XCC_ID << 32)
 constexpr int kDiagWaves = 8192;
 __device__ unsigned long long g_sit_wave[kDiagWaves][4];
+int diag_read_waves_impl(unsigned long long* out, int n) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (n > kDiagWaves) n = kDiagWaves;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sit_wave), sizeof(unsigned long long) * 4 * n) != hipSuccess) return -1;
+  return 0;
+}
 #endif
 #ifdef SIT_DIAG_PHASES
 // the fence makes the ship state live in registers at the timer, so arithmetic cannot be

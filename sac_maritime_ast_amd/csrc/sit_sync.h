@@ -687,6 +687,14 @@ __global__ __launch_bounds__(256) void k_env_steps_sync(const KArgs<T> a) {
   const bool act = lane < kSyncLanes && env < a.n_env;
   SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(smem + (LDSMAP ? (((size_t)a.map_bytes + 255) & ~size_t(255)) : 0));
   __syncthreads();   // constants copied, map staged
+#ifdef SIT_DIAG_PLACE
+  if (lane == 0 && blockIdx.x * 4 + w < kDiagWaves) {   // which SIMD each role's wave sits on
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);     // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);   // HW_REG_XCC_ID
+    unsigned long long* g = g_sit_wave[blockIdx.x * 4 + w];
+    g[0] = role; g[1] = blockIdx.x; g[2] = 0; g[3] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+  }
+#endif
   if (role == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, env, act);
   else if (role == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, env, act);
   else if (role == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, env, act);
