@@ -11,6 +11,7 @@ for r in $(seq 1 $rounds); do
       > gpurun_out/ab/${n}_$r.json 2> gpurun_out/ab/${n}_$r.err || { echo "$n failed"; tail -3 gpurun_out/ab/${n}_$r.err; exit 1; }
     python -c "
 import json; d=json.loads(open('gpurun_out/ab/${n}_$r.json').read().strip().splitlines()[-1])
-print('%-22s r%d %.4e env-steps/s  median launch %.3f ms' % ('$n', $r, d['value'], d['roofline']['launch_ms']['median']))"
+c5 = d.get('c5', {}).get('value')
+print('%-22s r%d %.4e env-steps/s  median launch %.3f ms  c5 %s' % ('$n', $r, d['value'], d['roofline']['launch_ms']['median'], '%.4e' % c5 if c5 else '-'))"
   done
 done

@@ -3,7 +3,7 @@
 (SIT_LIBRARY=build_diag/libsit_<name>.so; tools/ab_libs.sh), with the product's two-TU recipe
 (__graft_entry__.compile_library).
 
-  tools/build_variant.py <name> [--rev <git revision>] [hipcc flags ...]
+  tools/build_variant.py <name> [--rev <git revision>] [--f32 "<flags for the float32 TU only>"] [hipcc flags ...]
 
 --rev builds the sources of that revision (include/ and sac_maritime_ast_amd/csrc/ from git) instead
 of the working tree."""
@@ -21,10 +21,13 @@ name, rest = args[0], args[1:]
 rev = None
 if rest[:1] == ["--rev"]:
     rev, rest = rest[1], rest[2:]
+f32 = []
+if rest[:1] == ["--f32"]:
+    f32, rest = rest[1].split(), rest[2:]
 os.makedirs(os.path.join(ROOT, "build_diag"), exist_ok=True)
 out = os.path.join(ROOT, "build_diag", f"libsit_{name}.so")
 if rev is None:
-    g.compile_library(out, rest)
+    g.compile_library(out, rest, f32)
 else:
     with tempfile.TemporaryDirectory() as d:
         for sub in ("include", "sac_maritime_ast_amd/csrc"):
@@ -37,5 +40,5 @@ else:
                                            capture_output=True).stdout)
         g.ROOT, g.PKG = d, os.path.join(d, "sac_maritime_ast_amd")
         g.SOURCES = [os.path.join(g.PKG, "csrc", "sit_kernels.hip"), os.path.join(g.PKG, "csrc", "sit_steps_f32.hip")]
-        g.compile_library(out, rest)
+        g.compile_library(out, rest, f32)
 print("built", out)
