@@ -271,9 +271,11 @@ int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, do
                      void* stream);
 /* Debug builds (libsit_debug.so, compiled with -DSIT_DEBUG; no reference counterpart): every table
  * index the step kernels compute is bounds-checked; a failed check sets bit i of the returned word
- * (0 route-table row, 1 next-waypoint index, 2 route length, 3 spatial-index entry, 4 edge id,
- * 5 class-grid word, 6 mixed-cell record, 7 ship index) and its access is clamped into the table, so
- * the launch completes.  sit_debug_flags synchronises the device, returns the bits set since the last
+ * (0 route-table row, 1 next-waypoint index, 2 route length, 3 spatial-index entry or range, 4 edge
+ * id, 5 class-grid word, 6 mixed-cell record or live-edge range), and every table read it guards is
+ * clamped into its table (indices to a valid entry, ranges to their in-table part; the next-waypoint
+ * and route-length checks guard the route-table rows of bit 0), so the launch completes without an
+ * out-of-bounds access.  sit_debug_flags synchronises the device, returns the bits set since the last
  * call and clears them; release builds return 0.  sit_debug_build: 1 in a debug build. */
 int sit_debug_flags(uint32_t* flags);
 int32_t sit_debug_build(void);
@@ -334,16 +336,25 @@ typedef struct sit_rollout_args {
   /* Policy mode (action_ne == NULL, policy_action != NULL): the actions of sampling events come
    * from a policy evaluated between launches (the SAC actor, agent.select_action mode 1,
    * main_ast.py:344-349).  At a sampling event an env consumes policy_action[e] if
-   * policy_ready[e] != 0 (route angle a = policy_action[e] * pi/6, IW as in the synthetic
-   * sampler; policy_ready[e] is cleared); otherwise it takes no further step in this launch
-   * (its rows get status SIT_ST_NO_STEP and done 0) and queues a request: request_env[q] = e,
-   * request_noise[q] = N(0,1) from Philox4x32-10(key = seed, counter = (env_id, event, 0x504F, 0))
-   * (Box-Muller), q = atomicAdd(request_count) (requests beyond request_capacity are dropped
-   * and re-issued by the next launch).  The caller runs the policy on the queued envs'
-   * observations (state field last_obs) and writes policy_action / policy_ready before the
-   * next launch.  Per-env trajectories equal those of a synchronous per-step loop. */
+   * policy_ready[e] == SIT_POLICY_READY (route angle a = policy_action[e] * pi/6, IW as in the
+   * synthetic sampler); otherwise it takes no further step in this launch (its rows get status
+   * SIT_ST_NO_STEP and done 0).  At the end of the launch policy_ready[e] is SIT_POLICY_WAITING
+   * for every env stopped at a sampling event, SIT_POLICY_READY for an env holding an unused
+   * action, else 0.
+   * Admission (after the step kernel, same call, same stream; deterministic): the waiting envs
+   * enter the request queue oldest request first, ties by env id, at most request_capacity of
+   * them; request_age[e] counts the admission rounds env e has waited (kept by the library,
+   * zero-initialised by the caller).  An env that starts waiting in launch L is admitted at the
+   * latest in round L + ceil(n_env / request_capacity) - 1 (exact while ceil(n_env / request_capacity) < 16).  The
+   * queue rows are in env-id order: request_env[q] = e, request_obs[q] = the observation the env
+   * waits at (state field last_obs), request_noise[q] = N(0,1) from Philox4x32-10(key = seed,
+   * counter = (env_id, event, 0x504F, 0)) (Box-Muller), *request_count = rows.  Which envs step
+   * how many rows is therefore a function of (scenario, seed, request_capacity, n_steps, actions),
+   * never of scheduling.  The caller runs the policy on the queue and writes policy_action /
+   * policy_ready = SIT_POLICY_READY for the queued envs before the next launch (sit_policy_actor
+   * does both).  Per-env trajectories equal those of a synchronous per-step loop. */
   const void* policy_action;  /* real[n_env] in [-1, 1] */
-  int32_t* policy_ready;      /* int32[n_env] */
+  int32_t* policy_ready;      /* int32[n_env]: 0, SIT_POLICY_READY or SIT_POLICY_WAITING */
   int32_t* request_env;       /* int32[request_capacity] */
   void* request_noise;        /* real[request_capacity] */
   void* request_obs;          /* real[request_capacity][SIT_OBS_DIM]: the waiting env's state */
@@ -354,7 +365,10 @@ typedef struct sit_rollout_args {
    * path repeats its last logged row with the time updated (store_last_simulation_data), and
    * the fuel consumption accumulates over logged steps only (logging-only quantities). */
   void* log;
+  int32_t* request_age;       /* int32[n_env] (policy mode): admission rounds waited, see above */
 } sit_rollout_args;
+#define SIT_POLICY_READY 1    /* policy_ready: an action waits in policy_action[e] */
+#define SIT_POLICY_WAITING 2  /* policy_ready: the env stopped at a sampling event for its action */
 int sit_rollout(sit_handle* h, const sit_rollout_args* a, void* stream);
 size_t sit_rollout_args_size(void);
 /* Policy mode helper: the squashed Gaussian head of the actor (ast_core/distributions/normal.py:
@@ -375,9 +389,8 @@ int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t 
  *            W2 transposed [256 in][256 out], b2 [256], W3 [2][256], b3 [2]
  *   obs      real[capacity][SIT_OBS_DIM] (the request_obs rows of sit_rollout_args)
  *   served   int64[1] or NULL: += min(*request_count, capacity)
- *   clear_count int32[1] or NULL: set to 0 (one store, no grid-wide synchronisation).  With a
- *            two-slot request counter the caller alternates slots between launches: sit_rollout i
- *            appends to slot i%2, this call reads slot i%2 and clears slot (i+1)%2 for launch i+1. */
+ *   clear_count int32[1] or NULL: set to 0 (one store, no grid-wide synchronisation).  sit_rollout's
+ *            admission writes *request_count itself, so the build's sampler passes NULL. */
 #define SIT_ACTOR_HIDDEN 256
 #define SIT_ACTOR_WEIGHTS (SIT_ACTOR_HIDDEN * SIT_OBS_DIM + SIT_ACTOR_HIDDEN + SIT_ACTOR_HIDDEN * SIT_ACTOR_HIDDEN + \
                            SIT_ACTOR_HIDDEN + 2 * SIT_ACTOR_HIDDEN + 2)

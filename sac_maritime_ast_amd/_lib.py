@@ -31,6 +31,7 @@ ST_OBS_ENDPOINT, ST_OBS_HORIZON, ST_OBS_TERRAIN = 1 << 6, 1 << 7, 1 << 8
 ST_OBS_IW_TERMINAL, ST_OBS_NAVIGATION, ST_COLLISION = 1 << 9, 1 << 10, 1 << 11
 ST_TEST_DONE, ST_OBS_DONE, ST_ROUTE_OVERFLOW = 1 << 12, 1 << 13, 1 << 31
 ST_NO_STEP = 1 << 30
+SIT_POLICY_READY, SIT_POLICY_WAITING = 1, 2
 
 _D = c_double
 PARAM_FIELDS = [
@@ -83,7 +84,7 @@ class RolloutArgs(ctypes.Structure):
         ("policy_action", c_void_p), ("policy_ready", c_void_p), ("request_env", c_void_p),
         ("request_noise", c_void_p), ("request_obs", c_void_p), ("request_count", c_void_p),
         ("request_capacity", c_int32),
-        ("env_steps", c_void_p), ("log", c_void_p),
+        ("env_steps", c_void_p), ("log", c_void_p), ("request_age", c_void_p),
     ]
 
 

@@ -174,6 +174,209 @@ __global__ __launch_bounds__(256) void k_policy_actor(int cap, const float* __re
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Admission: the request queue of a policy-mode launch, built after the step kernel.
+//
+// The reference's loop never lets an env wait: every step gets an action (test_beds/main_ast.py:
+// 335-348, 378).  Here an env stopped at a sampling event waits until the actor has served it, and
+// the actor serves at most `cap` envs per launch; which ones is decided deterministically: oldest
+// request first (age = admission rounds waited, request_age[e]), ties by env id.  An env that starts
+// waiting in launch L is then admitted by round L + ceil(n / cap) - 1 (every round admits cap envs
+// that were ahead of it, and later requests never are), so per-env progress is a function of the
+// data and the capacity, not of wave scheduling (an atomic append decided it before round 4).
+//
+// The step kernel keeps the ages (age + 1 for an env that ends the launch waiting, else 0) and
+// publishes, per 64-env group, the waiting envs per age bucket (kAgeBuckets wave ballots,
+// publish_ages in sit_impl.h).  k_policy_admit then needs no global synchronisation: every block
+// reads the whole count table (32 KB at 32 768 envs, L2-resident), sums the buckets, finds the cutoff
+// bucket from the oldest down, and scans the groups in order for the first queue row of its own
+// groups and how many of their cutoff-bucket envs get in; each of its waves then ranks its group's
+// lanes with two ballots and writes their queue rows in env order with the observation each env
+// waits at (last_obs) and its event's normal draw, and clears the admitted envs' ages.  (A separate
+// one-block plan kernel measured 8.6 us per launch, latency-bound; redundant plans cost ~32 KB of L2
+// reads per block.)  Ages 1..kAgeBuckets-1 are ordered exactly; older ones share the last bucket
+// (env-id order there), which the FIFO bound keeps unreachable while ceil(n / cap) < kAgeBuckets.
+// ------------------------------------------------------------------------------------------
+constexpr int kAdmitThreads = 256;                             // 4 waves = 4 env groups per block
+constexpr int kAdmitGroups = kAdmitThreads / kAdmitGroup;
+constexpr int kAdmitPerThread = 2;                             // groups per thread and pass of the plan
+constexpr int kAdmitPass = kAdmitThreads * kAdmitPerThread;    // 512 groups = 32 768 envs per pass
+
+// exclusive prefix over the block (kAdmitThreads threads, thread order); *total = block sum.  s[8].
+__device__ __forceinline__ int admit_scan(int v, int* s, int* total) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+  constexpr int kW = kAdmitThreads / kWave;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == kWave - 1) s[w] = x;
+  __syncthreads();
+  int before = x - v, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kW; ++i) {
+    before += i < w ? s[i] : 0;
+    tot += s[i];
+  }
+  *total = tot;
+  __syncthreads();   // s reusable
+  return before;
+}
+
+// the age-bucket counts of group g (zeros past the last group)
+__device__ __forceinline__ void admit_row(const int32_t* __restrict__ counts, int g, int n_groups, int* row) {
+  if (g < n_groups) {
+    const int4* p = reinterpret_cast<const int4*>(counts + (size_t)g * kAgeBuckets);
+#pragma unroll
+    for (int i = 0; i < kAgeBuckets / 4; ++i) {
+      const int4 x = p[i];
+      row[4 * i] = x.x; row[4 * i + 1] = x.y; row[4 * i + 2] = x.z; row[4 * i + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < kAgeBuckets; ++b) row[b] = 0;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kAdmitThreads) void k_policy_admit(const KArgs<T> a, int cap,
+                                                                const int32_t* __restrict__ counts,
+                                                                int32_t* __restrict__ age, int32_t* __restrict__ req_env,
+                                                                int32_t* __restrict__ req_count, T* __restrict__ obs,
+                                                                T* __restrict__ noise) {
+  static_assert(kAgeBuckets % 4 == 0 && kAgeBuckets <= kWave, "bucket layout");
+  __shared__ int s[8];
+  __shared__ int tot[kAgeBuckets];
+  __shared__ int cut[2];
+  __shared__ int my_plan[kAdmitGroups][2];   // this block's groups: first queue row, admitted cutoff envs
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t >> 6;
+  const int n_env = a.n_env;
+  const int n_groups = (n_env + kAdmitGroup - 1) / kAdmitGroup;
+  // this wave's env (issued first: its load overlaps the plan)
+  const int g_me = blockIdx.x * kAdmitGroups + w;
+  const int e = g_me * kAdmitGroup + lane;
+  const bool in = e < n_env;
+  const int32_t a1 = in ? age[e] : 0;
+  if (t < kAgeBuckets) tot[t] = 0;
+  // bucket totals over every group
+  int rows[kAdmitPerThread][kAgeBuckets];
+#pragma unroll
+  for (int j = 0; j < kAdmitPerThread; ++j) admit_row(counts, t * kAdmitPerThread + j, n_groups, rows[j]);
+  int acc[kAgeBuckets];
+#pragma unroll
+  for (int b = 0; b < kAgeBuckets; ++b) acc[b] = rows[0][b] + rows[1][b];
+  for (int p0 = kAdmitPass; p0 < n_groups; p0 += kAdmitPass) {
+#pragma unroll
+    for (int j = 0; j < kAdmitPerThread; ++j) {
+      int r[kAgeBuckets];
+      admit_row(counts, p0 + t * kAdmitPerThread + j, n_groups, r);
+#pragma unroll
+      for (int b = 0; b < kAgeBuckets; ++b) acc[b] += r[b];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < kAgeBuckets; ++b) {
+    int x = acc[b];
+#pragma unroll
+    for (int off = kWave / 2; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+    if (lane == 0 && x) atomicAdd(&tot[b], x);
+  }
+  __syncthreads();
+  if (t == 0) {   // the cutoff, oldest bucket first
+    int total = 0;
+    for (int b = 0; b < kAgeBuckets; ++b) total += tot[b];
+    int bcut = 1, rem = 0x7fffffff;   // default: every waiting env is admitted
+    if (total > cap) {
+      int cum = 0;
+      for (int b = kAgeBuckets; b >= 1; --b) {
+        if (cum + tot[b - 1] >= cap) { bcut = b; rem = cap - cum; break; }
+        cum += tot[b - 1];
+      }
+    }
+    cut[0] = bcut; cut[1] = rem;
+    if (blockIdx.x == 0) *req_count = min(total, cap);
+  }
+  __syncthreads();
+  const int bcut = cut[0], rem = cut[1];
+  // every group in order: the cutoff-bucket envs before it and the queue rows before it
+  int pre_base = 0, row_base = 0;
+  for (int p0 = 0; p0 < n_groups; p0 += kAdmitPass) {
+    int cc[kAdmitPerThread], above[kAdmitPerThread];
+#pragma unroll
+    for (int j = 0; j < kAdmitPerThread; ++j) {
+      int r[kAgeBuckets];
+      if (p0 == 0) {
+#pragma unroll
+        for (int b = 0; b < kAgeBuckets; ++b) r[b] = rows[j][b];
+      } else {
+        admit_row(counts, p0 + t * kAdmitPerThread + j, n_groups, r);
+      }
+      cc[j] = 0; above[j] = 0;
+#pragma unroll
+      for (int b = 1; b <= kAgeBuckets; ++b) {
+        cc[j] += b == bcut ? r[b - 1] : 0;
+        above[j] += b > bcut ? r[b - 1] : 0;
+      }
+    }
+    int tc, ta;
+    int pre = pre_base + admit_scan(cc[0] + cc[1], s, &tc);
+    int cq[kAdmitPerThread], adm[kAdmitPerThread];
+#pragma unroll
+    for (int j = 0; j < kAdmitPerThread; ++j) {
+      cq[j] = max(0, min(cc[j], rem - pre));
+      adm[j] = above[j] + cq[j];
+      pre += cc[j];
+    }
+    int base = row_base + admit_scan(adm[0] + adm[1], s, &ta);
+#pragma unroll
+    for (int j = 0; j < kAdmitPerThread; ++j) {
+      const int g = p0 + t * kAdmitPerThread + j;
+      const int k = g - blockIdx.x * kAdmitGroups;
+      if (k >= 0 && k < kAdmitGroups) { my_plan[k][0] = base; my_plan[k][1] = cq[j]; }
+      base += adm[j];
+    }
+    pre_base += tc;
+    row_base += ta;
+  }
+  __syncthreads();
+  if (g_me >= n_groups) return;
+  // this wave's group: ranks by ballot, rows in env order
+  const int gbase = my_plan[w][0], gcq = my_plan[w][1];
+  const bool waiting = a1 > 0;
+  const int b = age_bucket(a1);
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int rank = (int)__popcll(__ballot(waiting && b == bcut) & lt);
+  const bool admit = waiting && (b > bcut || (b == bcut && rank < gcq));
+  const int row = gbase + (int)__popcll(__ballot(admit) & lt);
+  if (!admit) return;
+  T v[SIT_OBS_DIM];
+#pragma unroll
+  for (int k = 0; k < SIT_OBS_DIM; ++k) v[k] = a.st.last_obs[(size_t)k * n_env + e];
+  const uint32_t ev = a.st.event[e];
+  req_env[row] = e;
+  age[e] = 0;
+#pragma unroll
+  for (int k = 0; k < SIT_OBS_DIM; ++k) obs[(size_t)row * SIT_OBS_DIM + k] = v[k];
+  noise[row] = (T)sampler_normal(a.io.seed, (uint64_t)(a.io.env_id_offset + e), ev);
+}
+
+template <typename T>
+int launch_policy_admit(sit_handle* h, const sit_rollout_args* ra, hipStream_t stream) {
+  static_assert(kAdmitPerThread == 2, "admit_scan sums two groups per thread");
+  const int n_groups = (h->n_env + kAdmitGroup - 1) / kAdmitGroup;
+  KArgs<T> a = make_args<T>(h);
+  a.io.seed = ra->seed;
+  a.io.env_id_offset = ra->env_id_offset;
+  const int blocks = (n_groups + kAdmitGroups - 1) / kAdmitGroups;
+  hipLaunchKernelGGL(k_policy_admit<T>, dim3(blocks), dim3(kAdmitThreads), 0, stream, a, ra->request_capacity,
+                     admit_counts(h), ra->request_age, ra->request_env, ra->request_count, (T*)ra->request_obs,
+                     (T*)ra->request_noise);
+  return SIT_OK;
+}
+
 template <typename T>
 int launch_policy_actor(sit_handle* h, int cap, const float* w, const void* obs, const void* noise,
                         const int32_t* req_env, const int32_t* req_count, int det, void* act, int32_t* ready,

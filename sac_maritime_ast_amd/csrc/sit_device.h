@@ -102,7 +102,6 @@ enum DebugCheck {
   kDbgEdgeId = 4,        // an edge id >= the map's edge count
   kDbgClassWord = 5,     // a class-grid word outside the grid
   kDbgCellRecord = 6,    // a mixed-cell record or live-edge entry outside its table
-  kDbgShip = 7,          // a ship / env index outside the handle's population
 };
 #ifdef SIT_DEBUG
 namespace {
@@ -115,12 +114,24 @@ __device__ __forceinline__ int dbg_clamp(int i, int n, int id) {
   }
   return i;
 }
+// a range [first, first + cnt) of a table of n entries: the count that stays inside it
+__device__ __forceinline__ int dbg_span(int first, int cnt, int n, int id) {
+  if (first < 0 || cnt < 0 || first + cnt > n) {
+    atomicOr(&g_dbg_flags, 1u << id);
+    return first < 0 || first >= n ? 0 : max(0, min(cnt, n - first));
+  }
+  return cnt;
+}
 #define SIT_DCHECK(cond, id) do { if (!(cond)) atomicOr(&::sit::g_dbg_flags, 1u << (id)); } while (0)
 #define SIT_DCLAMP(i, n, id) ::sit::dbg_clamp((i), (n), (id))
+#define SIT_DSPAN(first, cnt, n, id) ::sit::dbg_span((first), (cnt), (n), (id))
 #else
 #define SIT_DCHECK(cond, id) do { } while (0)
 #define SIT_DCLAMP(i, n, id) (i)
+#define SIT_DSPAN(first, cnt, n, id) (cnt)
 #endif
+// an edge id read from the spatial index (checked and clamped in debug builds)
+#define SIT_DEDGE(m, i) SIT_DCLAMP((int)(i), (m).n_edge, kDbgEdgeId)
 
 constexpr int kWave = 64;         // CDNA wavefront
 #ifndef SIT_ENVS_PER_BLOCK
@@ -931,19 +942,20 @@ __device__ T distance_indexed(const Consts<T>& c, const Map<T>& m, T n, T e) {
   // cell record, so its edge loads depend on a single LDS read
   uint2 q = reinterpret_cast<const uint2*>(m.idx)[cell];
   const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (q.y >> 16);
-  const int ng = (int)((q.y >> 8) & 0xffu);
-  SIT_DCHECK(4 * ((int)(q.y >> 16) + ng) <= m.n_idx, kDbgIndexEntry);
-  T best = xmin(xmin(xmin(edge_dist2(m.edge[q.x & 0xffu], e, n), edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n)),
-                     xmin(edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n), edge_dist2(m.edge[q.x >> 24], e, n))),
-                edge_dist2(m.edge[q.y & 0xffu], e, n));
+  const int ng = SIT_DSPAN(4 * (int)(q.y >> 16), 4 * (int)((q.y >> 8) & 0xffu), m.n_idx, kDbgIndexEntry) / 4;
+  T best = xmin(xmin(xmin(edge_dist2(m.edge[SIT_DEDGE(m, q.x & 0xffu)], e, n),
+                          edge_dist2(m.edge[SIT_DEDGE(m, (q.x >> 8) & 0xffu)], e, n)),
+                     xmin(edge_dist2(m.edge[SIT_DEDGE(m, (q.x >> 16) & 0xffu)], e, n),
+                          edge_dist2(m.edge[SIT_DEDGE(m, q.x >> 24)], e, n))),
+                edge_dist2(m.edge[SIT_DEDGE(m, q.y & 0xffu)], e, n));
 #pragma unroll 1
   for (int g = 0; g < ng; ++g) {
     q = grp[g];
-    const T d0 = edge_dist2(m.edge[q.x & 0xffu], e, n);
-    const T d1 = edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n);
-    const T d2 = edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n);
-    const T d3 = edge_dist2(m.edge[q.x >> 24], e, n);
-    const T d4 = edge_dist2(m.edge[q.y & 0xffu], e, n);
+    const T d0 = edge_dist2(m.edge[SIT_DEDGE(m, q.x & 0xffu)], e, n);
+    const T d1 = edge_dist2(m.edge[SIT_DEDGE(m, (q.x >> 8) & 0xffu)], e, n);
+    const T d2 = edge_dist2(m.edge[SIT_DEDGE(m, (q.x >> 16) & 0xffu)], e, n);
+    const T d3 = edge_dist2(m.edge[SIT_DEDGE(m, q.x >> 24)], e, n);
+    const T d4 = edge_dist2(m.edge[SIT_DEDGE(m, q.y & 0xffu)], e, n);
     best = xmin(best, xmin(xmin(xmin(d0, d1), xmin(d2, d3)), d4));
   }
   return xsqrt(best);
@@ -974,34 +986,28 @@ __device__ __forceinline__ void pf_cell(const Consts<T>& c, const Map<T>& m, T n
 }
 template <typename T>
 __device__ __forceinline__ void pf_edges(const Map<T>& m, DistPf<T>& p) {
-  SIT_DCHECK((int)(p.q.x & 0xffu) < m.n_edge && (int)((p.q.x >> 8) & 0xffu) < m.n_edge &&
-             (int)((p.q.x >> 16) & 0xffu) < m.n_edge && (int)(p.q.x >> 24) < m.n_edge &&
-             (int)(p.q.y & 0xffu) < m.n_edge, kDbgEdgeId);
-  p.g[0] = m.edge[p.q.x & 0xffu];
-  p.g[1] = m.edge[(p.q.x >> 8) & 0xffu];
-  p.g[2] = m.edge[(p.q.x >> 16) & 0xffu];
-  p.g[3] = m.edge[p.q.x >> 24];
-  p.g[4] = m.edge[p.q.y & 0xffu];
+  p.g[0] = m.edge[SIT_DEDGE(m, p.q.x & 0xffu)];
+  p.g[1] = m.edge[SIT_DEDGE(m, (p.q.x >> 8) & 0xffu)];
+  p.g[2] = m.edge[SIT_DEDGE(m, (p.q.x >> 16) & 0xffu)];
+  p.g[3] = m.edge[SIT_DEDGE(m, p.q.x >> 24)];
+  p.g[4] = m.edge[SIT_DEDGE(m, p.q.y & 0xffu)];
 }
 template <typename T>
 __device__ __forceinline__ T pf_finish(const Map<T>& m, const DistPf<T>& p, T n, T e) {
   if (!p.ok) return distance_to_polys(m, n, e);
   const uint2* grp = reinterpret_cast<const uint2*>(m.idx) + (p.q.y >> 16);
-  const int ng = (int)((p.q.y >> 8) & 0xffu);
-  SIT_DCHECK(4 * ((int)(p.q.y >> 16) + ng) <= m.n_idx, kDbgIndexEntry);
+  const int ng = SIT_DSPAN(4 * (int)(p.q.y >> 16), 4 * (int)((p.q.y >> 8) & 0xffu), m.n_idx, kDbgIndexEntry) / 4;
   T best = xmin(xmin(xmin(edge_dist2(p.g[0], e, n), edge_dist2(p.g[1], e, n)),
                      xmin(edge_dist2(p.g[2], e, n), edge_dist2(p.g[3], e, n))),
                 edge_dist2(p.g[4], e, n));
 #pragma unroll 1
   for (int g = 0; g < ng; ++g) {
     const uint2 q = grp[g];
-    SIT_DCHECK((int)(q.x & 0xffu) < m.n_edge && (int)(q.x >> 24) < m.n_edge && (int)(q.y & 0xffu) < m.n_edge,
-               kDbgEdgeId);
-    const T d0 = edge_dist2(m.edge[q.x & 0xffu], e, n);
-    const T d1 = edge_dist2(m.edge[(q.x >> 8) & 0xffu], e, n);
-    const T d2 = edge_dist2(m.edge[(q.x >> 16) & 0xffu], e, n);
-    const T d3 = edge_dist2(m.edge[q.x >> 24], e, n);
-    const T d4 = edge_dist2(m.edge[q.y & 0xffu], e, n);
+    const T d0 = edge_dist2(m.edge[SIT_DEDGE(m, q.x & 0xffu)], e, n);
+    const T d1 = edge_dist2(m.edge[SIT_DEDGE(m, (q.x >> 8) & 0xffu)], e, n);
+    const T d2 = edge_dist2(m.edge[SIT_DEDGE(m, (q.x >> 16) & 0xffu)], e, n);
+    const T d3 = edge_dist2(m.edge[SIT_DEDGE(m, q.x >> 24)], e, n);
+    const T d4 = edge_dist2(m.edge[SIT_DEDGE(m, q.y & 0xffu)], e, n);
     best = xmin(best, xmin(xmin(xmin(d0, d1), xmin(d2, d3)), d4));
   }
   return xsqrt(best);
@@ -1016,11 +1022,11 @@ __device__ int pip_pair_indexed(const Consts<T>& c, const Map<T>& m, double n, d
   if (!(fb >= T(0) && fb < T(kBands))) return 0;   // beyond every edge's y-range
   const int b = (int)fb;
   uint32_t par0 = 0, onb0 = 0, par1 = 0, onb1 = 0;
-  const int k0 = m.idx[kBandBase + b], k1 = m.idx[kBandBase + b + 1];
-  SIT_DCHECK(k0 <= k1 && k1 <= m.n_idx, kDbgIndexEntry);
+  const int k0 = m.idx[kBandBase + b];
+  const int k1 = k0 + SIT_DSPAN(k0, (int)m.idx[kBandBase + b + 1] - k0, m.n_idx, kDbgIndexEntry);
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
-    const Edge<T> g = m.edge[m.idx[k]];
+    const Edge<T> g = m.edge[SIT_DEDGE(m, m.idx[k])];
     const uint32_t bit = 1u << g.poly;
     count_segment<double>(g.ax, g.ay, g.bx, g.by, x0, n, bit, par0, onb0);
     count_segment<double>(g.ax, g.ay, g.bx, g.by, x1, n, bit, par1, onb1);
@@ -1035,10 +1041,11 @@ __device__ bool pip_indexed(const Consts<T>& c, const Map<T>& m, double n, doubl
   if (!(fb >= T(0) && fb < T(kBands))) return false;
   const int b = (int)fb;
   uint32_t par = 0, onb = 0;
-  const int k0 = m.idx[kBandBase + b], k1 = m.idx[kBandBase + b + 1];
+  const int k0 = m.idx[kBandBase + b];
+  const int k1 = k0 + SIT_DSPAN(k0, (int)m.idx[kBandBase + b + 1] - k0, m.n_idx, kDbgIndexEntry);
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
-    const Edge<T> g = m.edge[m.idx[k]];
+    const Edge<T> g = m.edge[SIT_DEDGE(m, m.idx[k])];
     count_segment<double>(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
   }
   return (par & ~onb) != 0;
@@ -1073,10 +1080,10 @@ __device__ __forceinline__ int fine_class(const Consts<T>& c, const Map<T>& m, T
 #endif
 template <typename T>
 __device__ SIT_PIP_EXACT_INLINE bool pip_live_exact(const Edge<T>* edge, const uint8_t* live, int cnt,
-                                                         uint32_t par, double nd, double ed) {
+                                                         uint32_t par, double nd, double ed, int n_edge) {
   uint32_t onb = 0;
   for (int k = 0; k < cnt; ++k) {
-    const Edge<T> g = edge[live[k]];
+    const Edge<T> g = edge[SIT_DCLAMP((int)live[k], n_edge, kDbgEdgeId)];
     count_segment<double>(g.ax, g.ay, g.bx, g.by, ed, nd, 1u << g.poly, par, onb);
   }
   return (par & ~onb) != 0;
@@ -1122,13 +1129,13 @@ __device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t wor
   const int r = SIT_DCLAMP(m.frank[cell >> 4] + __popc(mixed & ((1u << ((cell & 15) * 2)) - 1u)), m.n_mixed,
                            kDbgCellRecord);
   const uint2 rec = m.crec[r];
-  const int first = (int)(rec.y & 0xffffu), cnt = (int)(rec.y >> 16);
-  SIT_DCHECK(first + cnt <= m.n_live, kDbgCellRecord);
+  const int first = (int)(rec.y & 0xffffu);
+  const int cnt = SIT_DSPAN(first, (int)(rec.y >> 16), m.n_live, kDbgCellRecord);
   if constexpr (kIsF32<T> && MODE == kPipFar) {
     uint32_t par = rec.x, onb = 0;
 #pragma unroll 1
     for (int k = 0; k < cnt; ++k) {
-      const Edge<T> g = m.edge[m.clive[first + k]];
+      const Edge<T> g = m.edge[SIT_DEDGE(m, m.clive[first + k])];
       count_segment<float>(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb);
     }
     return (par & ~onb) != 0;
@@ -1138,12 +1145,12 @@ __device__ __forceinline__ bool pip_cell(const Map<T>& m, int cell, uint32_t wor
       bool unsure = false;
 #pragma unroll 1
       for (int k = 0; k < cnt; ++k) {
-        const Edge<T> g = m.edge[m.clive[first + k]];
+        const Edge<T> g = m.edge[SIT_DEDGE(m, m.clive[first + k])];
         count_segment_f32(g.ax, g.ay, g.bx, g.by, e, n, 1u << g.poly, par, onb, unsure);
       }
       if (!unsure || !kKnifePip) return par != 0;
     }
-    return pip_live_exact(m.edge, m.clive + first, cnt, rec.x, nd, ed);
+    return pip_live_exact(m.edge, m.clive + first, cnt, rec.x, nd, ed, m.n_edge);
   }
 }
 

@@ -134,14 +134,12 @@ struct StepIO {
   int32_t* transition_count;
   int32_t transition_capacity;
   int32_t mask_horizon;
-  // policy mode (kPolicy): per-env action slots and the request queue of waiting envs
+  // policy mode (kPolicy): per-env action slots (the request queue is built after the launch by
+  // k_policy_admit, sit_actor.h)
   const T* policy_action;
   int32_t* policy_ready;
-  int32_t* request_env;
-  T* request_noise;
-  T* request_obs;
-  int32_t* request_count;
-  int32_t request_capacity;
+  int32_t* request_age;   // [n_env]: admission rounds waited (publish_ages)
+  int32_t* group_counts;  // [n_env / 64][kAgeBuckets]: waiting envs per age bucket (handle scratch)
   unsigned long long* env_steps;
   T* log;                 // [n_steps][SIT_LOG_ROWS][n_env] or null
 };
@@ -294,8 +292,9 @@ __device__ __forceinline__ double angle_or_nan(bool has, double a) {
 // the env step kernel: K steps of MultiShipRLEnv.step (+ optional auto-reset)
 //   MODE  : kExplicit = caller's action arrays, kSynth = synthetic AST sampler on device,
 //           kPolicy = actions from a policy run between launches (an env that reaches a
-//           sampling event without a fresh action waits for the rest of the launch and queues
-//           a request; the next launch consumes the action the policy wrote for it)
+//           sampling event without a fresh action waits for the rest of the launch; the
+//           admission kernel after the launch queues its request, and the next launch consumes
+//           the action the policy wrote for it)
 // ---------------------------------------------------------------------------------------
 #if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC) || defined(SIT_DIAG_PLACE)
 // Diagnostic builds only (tools/diag_paths.py, tools/diag_sync.py): [type][0..15] predicate path
@@ -452,6 +451,29 @@ __device__ __forceinline__ uint64_t opaque_seed(uint64_t seed) {
 #define SIT_PF_EDGES_EARLY 0   // 1: the candidate edges loaded right after guidance (measured slower)
 #endif
 constexpr int kExplicit = 0, kSynth = 1, kPolicy = 2;
+
+// Policy-mode admission (sit_actor.h): the step kernel keeps each env's request age (admission rounds
+// waited) and publishes per group of kAdmitGroup consecutive envs how many of them wait with each age
+// bucket (1 .. kAgeBuckets-1 exact, kAgeBuckets = that age or older)
+constexpr int kAgeBuckets = 16;
+constexpr int kAdmitGroup = 64;
+constexpr int32_t kAgeMax = 1 << 30;
+__device__ __forceinline__ int age_bucket(int32_t a) { return a < kAgeBuckets ? a : kAgeBuckets; }
+// the age after this launch (age + 1 if the env ends the launch waiting, else 0) and the env group's
+// bucket counts: one wave = one group of 64 envs (env = group * 64 + lane); every lane calls
+__device__ __forceinline__ void publish_ages(int32_t* age, int32_t* counts, int env, bool act, bool waiting,
+                                             int32_t age0) {
+  const int32_t a1 = (act && waiting) ? min(age0 + 1, kAgeMax) : 0;
+  if (act) age[env] = a1;
+  const int lane = threadIdx.x & (kWave - 1);
+  int mine = 0;
+#pragma unroll
+  for (int b = 1; b <= kAgeBuckets; ++b) {
+    const int c = (int)__popcll(__ballot(a1 > 0 && age_bucket(a1) == b));
+    if (lane == b - 1) mine = c;
+  }
+  if (lane < kAgeBuckets) counts[(size_t)(env / kAdmitGroup) * kAgeBuckets + lane] = mine;
+}
 // wave-uniform switches of the step loop (bits 0-4: the output arrays present)
 constexpr uint32_t kUfTrans = 1u << 5, kUfDoneCnt = 1u << 6, kUfAutoReset = 1u << 7, kUfMaskH = 1u << 8,
                    kUfCollBias = 1u << 9, kUfBlackout = 1u << 10;
@@ -504,12 +526,14 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   // policy mode: both lanes of an env track whether its next step is a sampling event
   bool need = false, ready = false, stalled = false;
   T pa = T(0);
+  int32_t age0 = 0;                  // policy mode: admission rounds waited (publish_ages)
   uint32_t n_stepped = 0;
   if (MODE == kPolicy && act) {
     const double samp0 = (double)a.st.env[0][env];
     need = a.st.ep_step[env] == 0 || (samp0 >= a.sc.ab_len[env] && a.st.stop[n_env + env] == 0);
-    ready = a.io.policy_ready[env] != 0;
+    ready = a.io.policy_ready[env] == SIT_POLICY_READY;
     pa = a.io.policy_action[env];
+    if (type == 1) age0 = a.io.request_age[env];
   }
   if (act) {
     for (int j = 0; j < lo_n; ++j) lo[j] = a.st.last_obs[(size_t)(lo_base + j) * n_env + env];
@@ -602,22 +626,10 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
     bool has_ang = false;
     bool ect_over = false;             // |e_ct| > e_tolerance, decided exactly (guidance_control)
     bool mech = false, blk = false;    // test ship: mechanical / blackout failure (decided pre-integration)
-    bool stall_now = false;
-    if (MODE == kPolicy && act && !stalled && need && !ready) {
-      // sampling event without an action: wait for the policy; the obstacle lane queues the
-      // request with this event's standard-normal draw (reparameterised sample, normal.py:96-101)
-      // and its half of the observation; the test lane adds its half after the exchange
-      stalled = stall_now = true;
-      if (type == 1) {
-        const int q = atomicAdd(a.io.request_count, 1);
-        x.slot[lane] = q;
-        if (q < a.io.request_capacity) {
-          a.io.request_env[q] = env;
-          a.io.request_noise[q] = (T)sampler_normal(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
-          for (int j = 0; j < 4; ++j) a.io.request_obs[(size_t)q * SIT_OBS_DIM + 6 + j] = lo[j];
-        }
-      }
-    }
+    // sampling event without an action: the env waits for the policy for the rest of the launch
+    // (both lanes decide alike); after the launch the admission kernel queues its request
+    // (k_policy_admit, sit_actor.h) from the state it stops in
+    if (MODE == kPolicy && act && !stalled && need && !ready) stalled = true;
     const bool live = act && !stalled;
     T sp = T(0), cp = T(1);
     if (live) xsincos(s.psi, &sp, &cp);    // heading trig of the step, off the guidance chain
@@ -839,11 +851,6 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
     if (MODE == kPolicy && act && !live && type == 0) {   // no step taken this row
       if (uf & 8) *p_st = SIT_ST_NO_STEP;
       if (uf & 4) *p_dn = 0;
-      if (stall_now) {
-        const int q = x.slot[lane];
-        if (q < a.io.request_capacity)
-          for (int j = 0; j < 6; ++j) a.io.request_obs[(size_t)q * SIT_OBS_DIM + j] = lo[j];
-      }
     }
     if (live) {
       const T dn = x.n[0][lane] - x.n[1][lane], de = x.e[0][lane] - x.e[1][lane];
@@ -948,7 +955,9 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   // ---------------- write back ----------------
   if (LOG && a.io.log && act) { a.st.fuel[0][sid] = f_me; a.st.fuel[1][sid] = f_el; a.st.fuel[2][sid] = f_tot; }
   if (MODE == kPolicy) {
-    if (act && type == 1) a.io.policy_ready[env] = ready ? 1 : 0;
+    if (act && type == 1) a.io.policy_ready[env] = ready ? SIT_POLICY_READY : (stalled ? SIT_POLICY_WAITING : 0);
+    static_assert(kEnvsPerBlock == kAdmitGroup || MODE != kPolicy, "one wave = one admission group");
+    if (type == 1) publish_ages(a.io.request_age, a.io.group_counts, env, act, stalled, age0);
     if (a.io.env_steps && type == 0) {   // env-steps executed: one atomic per wave
       unsigned long long v = act ? n_stepped : 0;
       for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
@@ -1157,7 +1166,7 @@ struct sit_handle {
   // scenario
   unsigned char* scen = nullptr;
   size_t scen_init = 0, scen_end_n = 0, scen_end_e = 0, scen_nw0 = 0, scen_ab_len = 0,
-         scen_ab_alpha = 0, scen_initial = 0, scen_bytes = 0;
+         scen_ab_alpha = 0, scen_initial = 0, scen_admit = 0, scen_bytes = 0;
   // map
   unsigned char* map = nullptr;
   int n_poly = 0, n_vert = 0;
@@ -1398,6 +1407,9 @@ KArgs<T> make_args(const sit_handle* h) {
   a.map_bytes = (int32_t)h->map_bytes;
   return a;
 }
+
+// policy-mode admission scratch: [n_groups][kAgeBuckets] counts, [n_groups][2] plan, header
+int32_t* admit_counts(const sit_handle* h) { return reinterpret_cast<int32_t*>(h->scen + h->scen_admit); }
 
 int ready(sit_handle* h) {
   if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");

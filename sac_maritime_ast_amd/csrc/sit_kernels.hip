@@ -263,6 +263,9 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
   h->scen_ab_len = so; so = align256(so + (size_t)n_env * 8);
   h->scen_ab_alpha = so; so = align256(so + (size_t)n_env * 8);
   h->scen_initial = so; so = align256(so + (size_t)n_env * SIT_OBS_DIM * rs);
+  // policy-mode admission scratch (sit_actor.h): per 64-env group the age-bucket counts and the plan
+  const size_t n_groups = ((size_t)n_env + kAdmitGroup - 1) / kAdmitGroup;
+  h->scen_admit = so; so = align256(so + (n_groups * (kAgeBuckets + 2) + 16) * 4);
   h->scen_bytes = so;
   if (setup_alloc(&h->blob, h->blob_bytes) != hipSuccess || setup_alloc(&h->scen, h->scen_bytes) != hipSuccess) {
     fail(nullptr, SIT_E_NOMEM, "hipMalloc of %zu + %zu bytes failed", h->blob_bytes, h->scen_bytes);
@@ -717,9 +720,9 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
   if (ra->policy_action && ra->action_ne)
     return fail(h, SIT_E_INVALID, "policy mode and explicit actions are exclusive");
   if (ra->policy_action && (!ra->policy_ready || !ra->request_env || !ra->request_noise || !ra->request_obs ||
-                            !ra->request_count || ra->request_capacity <= 0))
+                            !ra->request_count || !ra->request_age || ra->request_capacity <= 0))
     return fail(h, SIT_E_INVALID, "policy mode needs policy_ready, request_env, request_noise, "
-                                  "request_obs, request_count and a positive request_capacity");
+                                  "request_obs, request_count, request_age and a positive request_capacity");
   auto fill = [&](auto* io, auto* tag) {
     using R = std::remove_pointer_t<decltype(tag)>;
     io->n_steps = ra->n_steps; io->auto_reset = ra->auto_reset; io->seed = ra->seed;
@@ -730,20 +733,27 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     io->transitions = (R*)ra->transitions; io->transition_count = ra->transition_count;
     io->transition_capacity = ra->transition_capacity; io->mask_horizon = ra->mask_horizon;
     io->policy_action = (const R*)ra->policy_action; io->policy_ready = ra->policy_ready;
-    io->request_env = ra->request_env; io->request_noise = (R*)ra->request_noise;
-    io->request_obs = (R*)ra->request_obs;
-    io->request_count = ra->request_count; io->request_capacity = ra->request_capacity;
+    io->request_age = ra->request_age;
+    io->group_counts = ra->policy_action ? admit_counts(h) : nullptr;
     io->env_steps = reinterpret_cast<unsigned long long*>(ra->env_steps);
     io->log = (R*)ra->log;
   };
+  // policy mode: the step kernel, then the deterministic admission of the waiting envs into the
+  // request queue (k_policy_admit, sit_actor.h) on the same stream
   if (h->precision == SIT_F64) {
     StepIO<double> io{};
     fill(&io, (double*)nullptr);
-    return launch_steps<double>(h, io, (hipStream_t)stream);
+    rc = launch_steps<double>(h, io, (hipStream_t)stream);
+    if (rc == SIT_OK && ra->policy_action) rc = launch_policy_admit<double>(h, ra, (hipStream_t)stream);
+  } else {
+    StepIO<float> io{};
+    fill(&io, (float*)nullptr);
+    rc = launch_steps_f32(h, io, stream);
+    if (rc == SIT_OK && ra->policy_action) rc = launch_policy_admit<float>(h, ra, (hipStream_t)stream);
   }
-  StepIO<float> io{};
-  fill(&io, (float*)nullptr);
-  return launch_steps_f32(h, io, stream);
+  if (rc) return rc;
+  HIP_TRY(h, hipGetLastError());
+  return SIT_OK;
 }
 
 int sit_state_field(const sit_handle* h, int32_t id, const char** name, size_t* offset, int32_t* dtype,

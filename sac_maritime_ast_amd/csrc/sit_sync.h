@@ -20,9 +20,10 @@
 //
 // Policy mode (MODE == kPolicy, the sampler of samplers.PolicySampler): at a sampling event D1
 // consumes the env's action slot if the policy has filled it; otherwise the env takes no further
-// step in this launch (all four waves skip it: D1 publishes the decision before barrier A), D1
-// queues the request (env id, the event's standard-normal draw) and P0, which holds the env's
-// observation, writes the request's observation row and the ST_NO_STEP rows.
+// step in this launch (all four waves skip it: D1 publishes the decision before barrier A), P0 writes
+// the ST_NO_STEP rows, and D1 marks the env SIT_POLICY_WAITING at the end of the launch.  The request
+// queue is built after the launch, deterministically (k_policy_admit, sit_actor.h), from the state
+// the env stopped in.
 #pragma once
 
 #ifndef SIT_SYNC_LANES
@@ -62,8 +63,7 @@ constexpr uint32_t kPbTerrain = 1u << 0, kPbIw = 1u << 1, kPbArrive = 1u << 2, k
                    kPbColl = 1u << 4;   // kPbColl: the ship-ship collision, in the test ship's word (P0)
 // the episode ends: test ship arrival / horizon / terrain; obstacle horizon / terrain / IW; collision
 constexpr uint32_t kPbDoneTest = kPbArrive | kPbHorizon | kPbTerrain | kPbColl, kPbDoneObs = kPbHorizon | kPbTerrain | kPbIw;
-// the step's policy-mode decision (SyncSlot::q): the env steps / it stopped earlier in this launch;
-// q >= 0: it stops at this step and its request went to slot q of the queue
+// the step's policy-mode decision (SyncSlot::q): the env steps / it waits for its action
 constexpr int32_t kQLive = -1, kQStalled = -2;
 
 template <typename T>
@@ -119,12 +119,12 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   // policy mode: the env's action slot (D1), and whether the env stopped for the policy
   bool ready = false, stalled = false;
   T pa = T(0);
+  int32_t age0 = 0;              // policy mode (D1): admission rounds waited (publish_ages)
   // D1: the next sampling event's action and IW direction, drawn ahead (after the dynamics of the
   // step that consumed the previous one, or in the prologue) so that the event itself, on the
   // critical segment before barrier A, costs two multiply-adds
   double nx_act = 0.0;
   T nx_cs = T(0), nx_sn = T(0);
-  int32_t stall_q = -1;          // policy mode: the request slot whose noise is still to be drawn
   // explicit mode (D1): the caller's inputs of the next step, loaded one step ahead (the first step's
   // with the prologue's loads), so no global load sits on the segment before barrier A
   bool x_sac = false, x_init = false;
@@ -158,8 +158,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       ab_alpha = a.sc.ab_alpha[env];
       samp_limit = ieee_mul(ab_len, cs.x.theta);   // MSRL_env_ex.py:569
       if (MODE == kPolicy) {
-        ready = a.io.policy_ready[env] != 0;
+        ready = a.io.policy_ready[env] == SIT_POLICY_READY;
         pa = a.io.policy_action[env];
+        age0 = a.io.request_age[env];
       }
     }
   }
@@ -220,15 +221,11 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         sac = ep_step == 0 || ((double)samp >= ab_len && !s.stop);
         int32_t q = kQLive;
         if (MODE == kPolicy && sac && !ready) {
-          // no action yet: the env waits for the policy; queue the request (its noise is drawn
-          // after barrier A)
+          // no action yet: the env waits for the policy for the rest of the launch (the admission
+          // kernel after the launch queues its request, k_policy_admit)
           stalled = true;
           sac = false;
-          q = atomicAdd(a.io.request_count, 1);
-          if (q < a.io.request_capacity) {
-            a.io.request_env[q] = env;
-            stall_q = q;
-          }
+          q = kQStalled;
         } else if (sac) {                 // the action drawn ahead (draw_next)
           act_n = nx_act;
           if (MODE == kPolicy) ready = false;
@@ -248,11 +245,6 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     __syncthreads();   // A: positions (and the IW, and in policy mode the step's decision) published
     SY_MARK(1);
     if (MODE == kPolicy && TYPE == 0 && act && !stalled) stalled = xd.q[lane] != kQLive;
-    if (MODE == kPolicy && TYPE == 1 && stall_q >= 0) {
-      // the request's standard-normal draw of this event (the reparameterised sample, normal.py:96-101)
-      a.io.request_noise[stall_q] = (T)sampler_normal(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
-      stall_q = -1;
-    }
     if (act && !stalled) {
       T o_rpm, o_ect, o_pme = T(0);
       bool ect_over = false;
@@ -388,9 +380,11 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       a.st.ep_step[env] = ep_step;
       a.st.event[env] = event;
       a.st.episodes[env] = episodes;
-      if (MODE == kPolicy) a.io.policy_ready[env] = ready ? 1 : 0;
+      if (MODE == kPolicy) a.io.policy_ready[env] = ready ? SIT_POLICY_READY : (stalled ? SIT_POLICY_WAITING : 0);
     }
   }
+  static_assert(kSyncLanes == kAdmitGroup || MODE != kPolicy, "one wave = one admission group");
+  if (MODE == kPolicy && TYPE == 1) publish_ages(a.io.request_age, a.io.group_counts, env, act, stalled, age0);
   SY_MARK(13);   // epilogue (the wait at barrier C, the state write-back)
   SY_FLUSH(TYPE);
 }
@@ -473,8 +467,6 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       if (!live) {                     // no step in this row: the env waits for its action
         if (uf & 8) *p_st = SIT_ST_NO_STEP;
         if (uf & 4) *p_dn = 0;
-        if (q >= 0 && q < a.io.request_capacity)
-          for (int k = 0; k < SIT_OBS_DIM; ++k) a.io.request_obs[(size_t)q * SIT_OBS_DIM + k] = lo[k];
       } else {
         ++n_stepped;
       }

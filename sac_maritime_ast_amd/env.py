@@ -181,7 +181,9 @@ class VecMultiShipRLEnv:
         out["transitions"] ([capacity, 24]) and counted in out["transition_count"] ([1]); the count
         is zeroed first unless reset_transitions=False (several launches appending to one buffer).
         policy_io: the policy-mode buffers (see samplers.PolicySampler): actions of sampling events
-        come from a policy run between launches; waiting envs' rows carry status ST_NO_STEP."""
+        come from a policy run between launches; waiting envs' rows carry status ST_NO_STEP, and
+        after the launch the library admits waiting envs into the request queue, oldest request
+        first, ties by env id (include/sit.h, sit_rollout_args)."""
         n, K = self.n_env, int(n_steps)
         out = {} if out is None else out
         shapes = {"next_state": ((K, n, _lib.SIT_OBS_DIM), self.dtype), "reward": ((K, n), self.dtype),
@@ -229,7 +231,7 @@ class VecMultiShipRLEnv:
             if actions is not None:
                 raise ValueError("policy mode and explicit actions are exclusive")
             for k in ("policy_action", "policy_ready", "request_env", "request_noise", "request_obs",
-                      "request_count", "env_steps"):
+                      "request_count", "request_age", "env_steps"):
                 setattr(ra, k, policy_io[k].data_ptr())
             ra.request_capacity = int(policy_io["request_env"].numel())
         with torch.cuda.device(self.device):

@@ -11,13 +11,17 @@ Two action sources, as in ``agent.select_action(state, done, init, mode)`` (main
   evaluated in PyTorch-ROCm between fused K-step launches of the env kernel.
 
 Policy mode on the GPU: an env whose next step is a sampling event and that holds no fresh
-action stops for the rest of the launch and queues a request (its observation and a
-standard-normal draw keyed by (seed, env id, event)); after the launch the actor runs on the
-queued observations and scatters the squashed actions into per-env slots; the next launch
-consumes them.  Each env's trajectory is the one the synchronous per-step loop produces
-(oracle/sit_oracle.py ``OracleEnvs.policy_rollout``; tests/test_gpu_policy.py), independent of
-how envs are batched into launches.  ``OverlappedPolicySampler`` splits the envs into groups
-on separate HIP streams so one group's actor runs while the others' env kernels run.
+action stops for the rest of the launch.  After the launch the library admits the waiting envs
+into the request queue, oldest request first and ties by env id, at most ``request_capacity`` of
+them (each row: the env's observation and a standard-normal draw keyed by (seed, env id,
+event)); the actor runs on the queued observations and scatters the squashed actions into
+per-env slots; the next launch consumes them.  Each env's trajectory is the one the synchronous
+per-step loop produces (oracle/sit_oracle.py ``OracleEnvs.policy_rollout``;
+tests/test_gpu_policy.py), independent of how envs are batched into launches, and how many rows
+each env executes is a function of the data, the chunk and the capacity (an env waiting since
+launch L is served by round L + ceil(n_env / capacity) - 1), never of GPU scheduling.
+``OverlappedPolicySampler`` splits the envs into groups on separate HIP streams so one group's
+actor runs while the others' env kernels run.
 
 The converter from action to simulator input (``agent.convert_action_to_simu_input``) is absent
 from the reference; the build defines it: route angle a = action * pi/6 and
@@ -106,15 +110,15 @@ class PolicySampler:
     """Fused K-step launches in policy mode with the actor evaluated between launches.
 
     request_capacity bounds the envs served per launch (default n_env: every waiting env);
-    envs beyond it keep waiting and re-request on the next launch.  The actor runs on a fixed
-    number of rows (no host synchronisation); rows past the device-side request count are
+    envs beyond it keep waiting, oldest first, for the next admission round.  The actor runs on a
+    fixed number of rows (no host synchronisation); rows past the device-side request count are
     scattered into a dummy slot.
 
     With the reference's default actor architecture (``pack_actor_weights``) the whole actor runs as
-    one HIP kernel (sit_policy_actor), which also clears the request count for the next launch;
-    ``fused_actor=False`` or any other architecture evaluates the network with PyTorch-ROCm.  The
-    fused path reads a packed copy of the weights: after an optimizer step call
-    ``refresh_weights()`` (``act()`` does it by itself outside HIP-graph replays)."""
+    one HIP kernel (sit_policy_actor); ``fused_actor=False`` or any other architecture evaluates the
+    network with PyTorch-ROCm.  The fused path reads a packed copy of the weights: after an
+    optimizer step call ``refresh_weights()`` (``act()`` does it by itself outside HIP-graph
+    replays)."""
 
     def __init__(self, env: VecMultiShipRLEnv, policy: nn.Module, chunk: int = 32, seed: int = 25450,
                  env_id_offset: int = 0, request_capacity: int | None = None, mask_horizon: int = 600,
@@ -125,6 +129,8 @@ class PolicySampler:
         self.transition_capacity, self.deterministic = int(transition_capacity), deterministic
         n, dev, dt = env.n_env, env.device, env.dtype
         cap = int(request_capacity or n)
+        if cap <= 0:
+            raise ValueError("request_capacity must be positive")
         self.actor_dtype = actor_dtype or next(policy.parameters()).dtype
         self.io = {
             "policy_action": torch.zeros(n + 1, dtype=dt, device=dev),      # slot n: dummy
@@ -132,24 +138,20 @@ class PolicySampler:
             "request_env": torch.zeros(cap, dtype=torch.int32, device=dev),
             "request_noise": torch.zeros(cap, dtype=dt, device=dev),
             "request_obs": torch.zeros((cap, _lib.SIT_OBS_DIM), dtype=dt, device=dev),
+            # rows admitted by the last launch (written by the library's admission kernel)
+            "request_count": torch.zeros(1, dtype=torch.int32, device=dev),
+            # admission rounds each waiting env has waited (kept by the admission kernel)
+            "request_age": torch.zeros(n, dtype=torch.int32, device=dev),
             "env_steps": torch.zeros(1, dtype=torch.int64, device=dev),
         }
-        # two-slot request counter: launch i appends to slot i % 2 (io["request_count"] is a view
-        # of the current slot); the fused actor of launch i clears the other slot for launch i + 1
-        self._counts = torch.zeros(2, dtype=torch.int32, device=dev)
-        self._slot = 0
-        self.io["request_count"] = self._counts[0:1]
         self._rows = torch.arange(cap, device=dev, dtype=torch.int32)
-        self._one = torch.ones(cap, dtype=torch.int32, device=dev)
+        self._one = torch.full((cap,), _lib.SIT_POLICY_READY, dtype=torch.int32, device=dev)
         self.out: dict = {}
         self.served = torch.zeros(1, dtype=torch.int64, device=dev)   # policy evaluations used
         self._w = pack_actor_weights(policy) if fused_actor and self.actor_dtype == torch.float32 else None
         if self._w is not None:
             self._w = self._w.to(dev)
             self._w_version = self._weights_version()
-        # the counter slot the next launch appends to was cleared by the previous launch's actor (the
-        # fused actor clears the other slot); an act() outside launch() leaves it holding a count
-        self._slot_clean = True
 
     @property
     def fused(self) -> bool:
@@ -176,10 +178,6 @@ class PolicySampler:
         events: optional (start, end) torch.cuda.Event pair recorded around the env kernel.
         first: the launch starts a new batch of replay transitions (their count is zeroed); later
         launches of a batch append to it, so a HIP graph of several launches keeps all of them."""
-        p = self._slot
-        self.io["request_count"] = self._counts[p:p + 1]
-        if self._w is None or not self._slot_clean:
-            self.io["request_count"].zero_()
         if events is not None:
             events[0].record(torch.cuda.current_stream(self.env.device))
         self.env.rollout(self.chunk, seed=self.seed, env_id_offset=self.env_id_offset, out=self.out,
@@ -188,17 +186,14 @@ class PolicySampler:
         if events is not None:
             events[1].record(torch.cuda.current_stream(self.env.device))
         self.act()
-        self._slot_clean = True
-        self._slot ^= 1
         return self.out
 
     def capture(self, n_launch: int = 2, want=("next_state", "reward", "done", "status", "action")):
-        """Record `n_launch` launches (env kernel + actor) into one HIP graph; replay() then runs
-        them with a single submission (the per-launch host work of ctypes and ~10 torch ops
-        otherwise bounds short chunks).  The output buffers are those of the last launch.
-        n_launch must be even (the request-counter slots alternate per launch)."""
-        if n_launch % 2:
-            raise ValueError("capture an even number of launches (two-slot request counter)")
+        """Record `n_launch` launches (env kernel + admission + actor) into one HIP graph; replay()
+        then runs them with a single submission (the per-launch host work of ctypes and ~10 torch
+        ops otherwise bounds short chunks).  The output buffers are those of the last launch."""
+        if n_launch < 1:
+            raise ValueError("capture at least one launch")
         self.launch(want)                     # allocate every buffer outside the capture
         self.launch(want)
         torch.cuda.synchronize(self.env.device)
@@ -220,7 +215,6 @@ class PolicySampler:
         (sit_policy_apply), or for policies without a `.net` (mu, log_sigma) trunk forward() and a
         device-side scatter."""
         io, env = self.io, self.env
-        self._slot_clean = False             # launch() marks it clean again after its own act()
         if self._w is not None:
             if not torch.cuda.is_current_stream_capturing() and self._weights_version() != self._w_version:
                 self.refresh_weights()
@@ -229,7 +223,7 @@ class PolicySampler:
                           io["request_noise"].data_ptr(), io["request_env"].data_ptr(),
                           io["request_count"].data_ptr(), int(bool(self.deterministic)),
                           io["policy_action"].data_ptr(), io["policy_ready"].data_ptr(), self.served.data_ptr(),
-                          self._counts[1 - self._slot:2 - self._slot].data_ptr(), env._stream())
+                          None, env._stream())
             return
         obs = io["request_obs"] if self.actor_dtype == env.dtype else io["request_obs"].to(self.actor_dtype)
         net = getattr(self.policy, "net", None)
@@ -279,9 +273,9 @@ class OverlappedPolicySampler:
 
     def capture(self, n_launch: int = 2, want=("next_state", "reward", "done", "status", "action")):
         """One HIP graph holding `n_launch` rounds of every group (forked onto the groups'
-        streams inside the capture, joined at the end); n_launch even (PolicySampler.capture)."""
-        if n_launch % 2:
-            raise ValueError("capture an even number of launches (two-slot request counter)")
+        streams inside the capture, joined at the end)."""
+        if n_launch < 1:
+            raise ValueError("capture at least one launch")
         self.launch(want)
         self.launch(want)
         torch.cuda.synchronize(self.streams[0].device)

@@ -199,9 +199,8 @@ def test_fused_actor_matches_torch_float64(precision, deterministic):
     assert sm.fused
     io = sm.io
     checked = 0
+    clear = torch.full((1,), 7, dtype=torch.int32, device=DEV)
     for it in range(6):
-        io["request_count"].zero_()
-        sm._counts[1].fill_(7)              # the other slot: cleared by the actor
         env.rollout(sm.chunk, seed=sm.seed, env_id_offset=0, out=sm.out, policy_io=io)
         torch.cuda.synchronize()
         count = min(int(io["request_count"].item()), io["request_env"].numel())
@@ -210,9 +209,16 @@ def test_fused_actor_matches_torch_float64(precision, deterministic):
         envs = io["request_env"][:count].long().clone()
         served0 = int(sm.served.item())
         io["policy_ready"].zero_()
-        sm.act()
+        if it == 0:     # the ABI's optional clear_count store
+            with torch.cuda.device(env.device):
+                env._call("sit_policy_actor", int(sm._rows.numel()), sm._w.data_ptr(), io["request_obs"].data_ptr(),
+                          io["request_noise"].data_ptr(), io["request_env"].data_ptr(),
+                          io["request_count"].data_ptr(), int(bool(deterministic)), io["policy_action"].data_ptr(),
+                          io["policy_ready"].data_ptr(), sm.served.data_ptr(), clear.data_ptr(), env._stream())
+        else:
+            sm.act()
         torch.cuda.synchronize()
-        assert int(sm._counts[1].item()) == 0
+        assert int(clear.item()) == 0
         assert int(sm.served.item()) == served0 + count
         with torch.no_grad():
             ref = ref_pol(obs, noise, deterministic=deterministic)[0][:, 0]
@@ -270,6 +276,7 @@ def _policy_io(n_env, cap, dtype):
           "request_noise": torch.zeros(cap, dtype=dtype, device=DEV),
           "request_obs": torch.zeros((cap, _lib.SIT_OBS_DIM), dtype=dtype, device=DEV),
           "request_count": torch.zeros(1, dtype=torch.int32, device=DEV),
+          "request_age": torch.zeros(n_env, dtype=torch.int32, device=DEV),
           "env_steps": torch.zeros(1, dtype=torch.int64, device=DEV)}
     return io
 
@@ -358,9 +365,11 @@ def test_f32_policy_mode_step_vs_oracle():
             assert np.array_equal(post[k][:, live], ref[k][:, live].astype(post[k].dtype)), f"depth {depth}: {k}"
         for k in so.ENV_INT:
             assert np.array_equal(post[k][live].astype(np.int64), ref[k][live].astype(np.int64)), f"depth {depth}: {k}"
-        # the consumed action slots are cleared, the others keep their flag
+        # the consumed action slots are cleared, the unused ones keep their flag, the waiting envs
+        # are marked SIT_POLICY_WAITING
         rd = io["policy_ready"][:n_env].cpu().numpy()
-        assert np.array_equal(rd, (ready & ~need).astype(np.int32)), f"depth {depth}: policy_ready"
+        want_rd = np.where(wait, _lib.SIT_POLICY_WAITING, (ready & ~need).astype(np.int32) * _lib.SIT_POLICY_READY)
+        assert np.array_equal(rd, want_rd), f"depth {depth}: policy_ready"
         # replay transitions of the stepping envs' events (per env id; the kernel appends with atomics)
         cnt = int(out["transition_count"].item())
         got = out["transitions"][:cnt].cpu().numpy().astype(np.float64)
@@ -383,7 +392,9 @@ def test_f32_policy_mode_step_vs_oracle():
         q = int(io["request_count"].item())
         assert q == int(wait.sum()), f"depth {depth}: {q} requests for {int(wait.sum())} waiting envs"
         renv = io["request_env"][:q].cpu().numpy()
-        assert np.array_equal(np.sort(renv), np.nonzero(wait)[0]), f"depth {depth}: request env ids"
+        # the admission queues the waiting envs in env-id order (all of them: capacity = n_env)
+        assert np.array_equal(renv, np.nonzero(wait)[0]), f"depth {depth}: request env ids"
+        assert not io["request_age"].any(), f"depth {depth}: admitted envs keep an age"
         robs = io["request_obs"][:q].cpu().numpy().astype(np.float64)
         assert np.array_equal(robs, st["last_obs"].T[renv]), f"depth {depth}: request observations"
         noise = so.sampler_normal(seed, renv.astype(np.uint64), st["event"][renv])
@@ -448,28 +459,148 @@ def test_f32_c5_size_fused_actor_graph_replay():
         assert s > 0.8 * 3 * per_graph * chunk * n, stepped
     for s in samplers:
         assert int(s.served.item()) > n
-    # batching independence (eager launches; the graph's launches are the same kernels)
-    m = 512
-    envs = []
+    # batching independence (eager launches; the graph's launches are the same kernels): the first
+    # 512 envs as part of the 16 384-env handle and as a 512-env handle execute identical rows; each
+    # handle's per-env progress obeys the admission's FIFO bound and is reproducible
+    m, n_launch = 512, 12
+    envs, counts = [], []
     for nn in (n, m):
         env = VecMultiShipRLEnv(scenario=make_scenario(nn, cap=48, seed=25450, env_offset=0), precision=32,
                                 device=DEV)
         env.reset()
         env.init_step()
         sm = PolicySampler(env, pol, chunk=chunk, seed=SEED, env_id_offset=0, request_capacity=nn // 4)
-        outs = []
-        for _ in range(12):
+        outs, stalled = [], []
+        for _ in range(n_launch):
             o = sm.launch()
             torch.cuda.synchronize()
             outs.append({k: o[k][:, :m].cpu().numpy().copy() for k in ("next_state", "reward", "status")})
+            st = o["status"].to(torch.int64) & 0xFFFFFFFF
+            stalled.append(((st & _lib.ST_NO_STEP) != 0).all(0).cpu().numpy())
         envs.append(_executed_rows(outs, m))
+        _assert_fifo_bound(np.stack(stalled), nn, nn // 4)
     big, small = envs
     compared = 0
     for e in range(m):
         k = min(len(big[e]), len(small[e]))
-        assert k >= 200, f"env {e}: {k} rows"
+        assert k >= 1, f"env {e}: no rows"
         for i in range(k):
             assert np.array_equal(big[e][i][0], small[e][i][0]) and big[e][i][1] == small[e][i][1] \
                 and big[e][i][2] == small[e][i][2], f"env {e} row {i}"
         compared += k
-    assert compared > 100000
+    assert compared > 100000, compared
+
+
+def _assert_fifo_bound(stalled, n_env, cap):
+    """stalled [launch, env]: the env took no step in the launch.  A request made in launch L is
+    admitted by round L + ceil(n/cap) - 1 and its action consumed in the next launch, so an env
+    takes no step in at most ceil(n/cap) consecutive launches (include/sit.h, sit_rollout_args)."""
+    bound = -(-n_env // cap)
+    run = np.zeros(stalled.shape[1], dtype=np.int64)
+    worst = np.zeros_like(run)
+    for row in stalled:
+        run = np.where(row, run + 1, 0)
+        worst = np.maximum(worst, run)
+    assert worst.max() <= bound, f"an env waited {worst.max()} launches in a row (bound {bound})"
+    return worst
+
+
+def _admission_model(ready_after, age_before, cap):
+    """The admission rule in numpy: waiting envs (policy_ready == SIT_POLICY_WAITING) age by one round;
+    the oldest `cap` (ties by env id; ages of 16 and more share one bucket) are queued in env-id order and
+    their age reset; the others keep waiting with their age; envs not waiting have age 0."""
+    n = age_before.size
+    wait = ready_after[:n] == _lib.SIT_POLICY_WAITING
+    age = np.where(wait, np.minimum(age_before.astype(np.int64) + 1, 1 << 30), 0)
+    cand = np.nonzero(wait)[0]
+    order = cand[np.lexsort((cand, -np.minimum(age[cand], 16)))]
+    adm = np.sort(order[:cap])
+    age[adm] = 0
+    return adm, age
+
+
+def _run_overflowing(n, cap, chunk, n_launch, pol, check_model):
+    """n envs, capacity cap < the demand, eager launches; per launch the admitted queue is checked
+    against _admission_model (check_model).  Returns the per-env executed-row counts and the
+    [launch, env] fully-stalled matrix."""
+    env = VecMultiShipRLEnv(scenario=make_scenario(n, cap=48, seed=77), precision=32, device=DEV)
+    env.reset()
+    env.init_step()
+    sm = PolicySampler(env, pol, chunk=chunk, seed=SEED, request_capacity=cap)
+    io = sm.io
+    rows = np.zeros(n, dtype=np.int64)
+    stalled, overflowed = [], 0
+    for _ in range(n_launch):
+        age0 = io["request_age"].cpu().numpy().copy()
+        env.rollout(chunk, seed=SEED, out=sm.out, want=("next_state", "reward", "done", "status", "action"),
+                    policy_io=io)
+        torch.cuda.synchronize()
+        if check_model:
+            ready = io["policy_ready"].cpu().numpy()
+            adm, age = _admission_model(ready, age0, cap)
+            q = int(io["request_count"].item())
+            assert q == adm.size, (q, adm.size)
+            assert np.array_equal(io["request_env"][:q].cpu().numpy(), adm)
+            assert np.array_equal(io["request_age"].cpu().numpy(), age)
+            overflowed += int((ready[:n] == _lib.SIT_POLICY_WAITING).sum()) - q
+        sm.act()
+        st = sm.out["status"].to(torch.int64) & 0xFFFFFFFF
+        live = (st & _lib.ST_NO_STEP) == 0
+        rows += live.sum(0).cpu().numpy()
+        stalled.append((~live).all(0).cpu().numpy())
+    if check_model:
+        assert overflowed > 0, "the queue never overflowed"
+    assert int(rows.sum()) == int(sm.env_steps.item())
+    return rows, np.stack(stalled)
+
+
+def test_f32_policy_admission_is_deterministic_and_fifo():
+    """An overflowing request queue (capacity n/8): the admitted rows of every launch equal the
+    admission rule's (oldest request first, ties by env id; _admission_model), two runs from the same
+    start execute identical per-env row counts, and no env waits longer than the FIFO bound."""
+    n, chunk, n_launch = 4096, 32, 16
+    cap = n // 8
+    pol = make_policy256(DEV)
+    rows1, st1 = _run_overflowing(n, cap, chunk, n_launch, pol, check_model=True)
+    rows2, st2 = _run_overflowing(n, cap, chunk, n_launch, pol, check_model=False)
+    assert np.array_equal(rows1, rows2), "per-env progress differs between two identical runs"
+    assert np.array_equal(st1, st2)
+    worst = _assert_fifo_bound(st1, n, cap)
+    assert worst.max() >= 2, "the test did not exercise waiting across launches"
+    print(f"admission: rows/env min {rows1.min()} mean {rows1.mean():.1f}, longest wait {worst.max()} launches")
+
+
+def test_f64_intermediate_waypoint_sampler_switches_to_policy():
+    """IntermediateWaypointSampler (the reference's empty ast_core sampler): random IWs (mode 0, device
+    Philox draws) for the first start_steps env-steps, then the policy (mode 1) — main_ast.py:335-348.
+    Per env: the random phase equals OracleEnvs.rollout, the policy phase equals OracleEnvs.policy_rollout
+    continued from the same state (float64, 1e-9)."""
+    from sac_maritime_ast_amd.samplers import IntermediateWaypointSampler
+    n_env, chunk, n_rand, n_pol = 64, 16, 6, 30
+    sc = make_scenario(n_env, cap=32, seed=13)
+    env = VecMultiShipRLEnv(scenario=sc, precision=64, device=DEV)
+    env.reset()
+    env.init_step()
+    ims = IntermediateWaypointSampler(env, make_policy(torch.float64, DEV), chunk=chunk, seed=SEED,
+                                      start_steps=n_rand * chunk * n_env, request_capacity=n_env // 2)
+    rand_rows, pol_rows = [], []
+    for i in range(n_rand + n_pol):
+        out = ims.launch()
+        torch.cuda.synchronize()
+        snap = {k: v.cpu().numpy().copy() for k, v in out.items() if k != "done_count"}
+        (rand_rows if i < n_rand else pol_rows).append([snap])
+    assert ims.policy_sampler.served.item() > 0
+    o = so.OracleEnvs(dict(so.DEFAULT_PARAMS), sc.routes, sc.n_wpt, sc.init, sc.polys)
+    o.reset()
+    o.init_step()
+    r = o.rollout(n_rand * chunk, SEED)
+    got = {k: np.concatenate([l[0][k] for l in rand_rows]) for k in ("next_state", "reward", "done", "status")}
+    err = np.abs(got["next_state"] - r["next_state"]) / np.maximum(np.abs(r["next_state"]), OBS_SCALE)
+    assert err.max() <= 1e-9, f"random phase rel err {err.max():.3e}"
+    assert np.array_equal(got["done"].astype(bool), r["done"])
+    assert np.array_equal(got["status"].astype(np.int64) & 0xFFFFFFFF, r["status"].astype(np.int64))
+    seq = per_env(pol_rows, 0, n_env)
+    n = min(len(x) for x in seq["reward"])
+    assert n >= 200, n
+    ref = o.policy_rollout(n, SEED, oracle_policy_fn(make_policy(torch.float64, "cpu")))
+    compare(seq, ref, n_env, n)

@@ -10,6 +10,7 @@ while [ $# -gt 0 ]; do
   cmd=()
   while [ $# -gt 0 ] && [ "$1" != "---" ]; do cmd+=("$1"); shift; done
   [ $# -gt 0 ] && shift
+  mkdir -p "gpurun_out/$(dirname "$name")"
   start=$(date +%s)
   timeout -k 10 "$to" "${cmd[@]}" > "gpurun_out/$name.log" 2>&1
   rc=$?
