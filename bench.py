@@ -72,9 +72,9 @@ def parse():
     ap.add_argument("--cpu-baseline-workers", type=int, default=16,
                     help="single-threaded oracle processes (the GPU box's CPU share is 16 cores per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--transitions", action="store_true",
-                    help="N = 1: write the replay transitions too (every rank writes them at N > 1)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="skip the replay-transition stream (by default every rank, N = 1 included, writes "
+                         "its sampling events' transitions and the learner gathers them)")
     ap.add_argument("--launch-trace", action="store_true", help="print every launch's kernel ms to stderr")
     ap.add_argument("--no-c5", action="store_true", help="rollout mode: skip the config C5 (policy) line")
     ap.add_argument("--c5-steps", type=int, default=32 * 16 * 16, help="timed steps of the C5 line")
@@ -363,8 +363,10 @@ def bench_rollout(args, rank, world, dev):
     # headroom; floor n_env so the synchronised episode start (one event per env) always fits.
     # Records beyond it are counted and reported ("dropped").
     tcap = max(n_env, n_env * chunk // 192)
-    gather = AsyncTransitionGather(tcap, 24, env.dtype, dev, world) if (world > 1 and not args.no_gather) else None
-    local_tr = args.transitions and gather is None
+    # every N, N = 1 included, times the same work: the kernel writes the transitions and the learner
+    # gathers them (at N = 1 rank 0 is the learner: the count crosses to the host, no record moves)
+    gather = AsyncTransitionGather(tcap, 24, env.dtype, dev, world) if (args.mode == "rollout" and not args.no_gather) \
+        else None
     out = {}
     launch_no = [0]
 
@@ -394,7 +396,7 @@ def bench_rollout(args, rank, world, dev):
             if ev_pair:
                 ev_pair[0].record(stream)
             env.rollout(chunk, seed=args.seed, env_id_offset=offset, out=out,
-                        transition_capacity=tcap if (gather or local_tr) else 0)
+                        transition_capacity=tcap if gather else 0)
             if ev_pair:
                 ev_pair[1].record(stream)
             if gather:     # counts now, the valid records once this launch's counts are on the host
@@ -447,14 +449,12 @@ def bench_rollout(args, rank, world, dev):
         "roofline": rl,
         "roofline_valu": roofline_valu(kern_ms, pmc, n_env, chunk) if args.mode == "rollout" else None,
     }
-    if local_tr:
-        cnt = int(out["transition_count"].item())
-        res["config"]["transitions"] = {"records_last_launch": cnt, "capacity": tcap, "dropped_last_launch": max(0, cnt - tcap)}
     if gather is not None:
         stats = torch.tensor([gather.gathered - gathered0, gather.dropped() - dropped0], dtype=torch.float64,
                              device=dev)
         res["config"]["rccl_transition_gather"] = {
-            "to": "rank 0 (learner)", "records_gathered": int(stats[0].item()),
+            "to": "rank 0 (learner)" + (" (N = 1: the learner's own records, no transfer)" if world == 1 else ""),
+            "records_gathered": int(stats[0].item()),
             "records_dropped": int(stats[1].item()), "capacity_per_rank_launch": tcap,
             "bytes_per_record": 24 * rs, "pipelining": "count all-gather behind each launch; valid records "
                                                        "point-to-point once the next launch is enqueued"}
@@ -473,10 +473,10 @@ def bench_policy(args, rank, world, dev):
 
     n_env, G, chunk = args.n_env, args.groups, args.chunk
     per = n_env // G
-    per_graph = max(2, min(args.graph_launches, max(2, args.steps // chunk)) // 2 * 2)   # even: 2-slot counter
-    gathering = world > 1 and not args.no_gather
+    per_graph = max(1, min(args.graph_launches, max(1, args.steps // chunk)))
+    gathering = not args.no_gather
     # transitions of one graph replay per group: 1 per ~390 env-steps measured (C3), 1 per 96 here
-    tcap = per * chunk * per_graph // 96 if (gathering or args.transitions) else 0
+    tcap = per * chunk * per_graph // 96 if gathering else 0
     torch.manual_seed(args.seed)
     policy = GaussianPolicy(hidden=(256, 256)).to(dev)
     samplers = []

@@ -300,6 +300,17 @@ int sit_init_step(sit_handle* h, const uint8_t* env_mask, void* stream);
 int sit_step(sit_handle* h, const void* action_ne, const uint8_t* sac_update,
              const uint8_t* init, void* next_state, void* reward, uint8_t* done,
              uint32_t* status, int32_t* done_count, void* stream);
+/* MultiShipRLEnv.step with HOST arrays (the scalar drop-in, compat.MultiShipRLEnv.step; the reference
+ * API is synchronous): the same step as sit_step, with the arrays above in host memory and
+ *   log   real[SIT_LOG_ROWS][n_env] or NULL: the step's trajectory-log row (sit_rollout_args.log)
+ *   state sit_state_bytes() bytes or NULL: the state blob after the step (sit_get_state)
+ * The inputs go into the handle's pinned, coherent host staging, which the step kernel reads and
+ * writes directly (no copy call); one launch, one copy of the state blob when asked, one
+ * synchronisation of `stream`, then the outputs are copied to the caller's arrays.  Any output may be
+ * NULL.  Returns after the step has completed. */
+int sit_step_host(sit_handle* h, const void* action_ne, const uint8_t* sac_update, const uint8_t* init,
+                  void* next_state, void* reward, uint8_t* done, uint32_t* status, void* log, void* state,
+                  void* stream);
 
 /* K fused steps.  With action_ne == NULL the synthetic AST sampler drives the obstacle
  * ship: a sampling event happens on the first step of an episode and

@@ -121,6 +121,8 @@ SIGNATURES = {
     "sit_init_step": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "sit_step": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p]),
+    "sit_step_host": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p]),
     "sit_rollout": (c_int32, [c_void_p, POINTER(RolloutArgs), c_void_p]),
     "sit_state_nfields": (c_int32, []),
     "sit_state_field": (c_int32, [c_void_p, c_int32, POINTER(c_char_p), POINTER(c_size_t),

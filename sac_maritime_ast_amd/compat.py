@@ -32,6 +32,8 @@ the next step.
 from __future__ import annotations
 
 import math
+from ctypes import c_void_p
+from functools import lru_cache
 from types import SimpleNamespace
 
 import numpy as np
@@ -44,6 +46,8 @@ from .env import VecMultiShipRLEnv
 from .scenario import Scenario, polygons
 from .status import status_string
 from .trajectory import LOG_KEYS, REWARD_SERIES
+
+_status_string = lru_cache(maxsize=8192)(status_string)   # the per-step status decode, memoised
 
 _REQUIRED = object()
 
@@ -319,7 +323,7 @@ class _ShipModelView(_View):
         "forward_speed": _real("surge"), "sideways_speed": _real("sway"), "yaw_rate": _real("yaw_rate"),
         "int": (lambda env, t: _IntView(env, t),),
         "ship_machinery_model": (lambda env, t: _MachineryView(env, t),),
-        "simulation_results": (lambda env, t: env._sim_results[t],),
+        "simulation_results": (lambda env, t: (env._flush(), env._sim_results[t])[1],),
         **{f"init_{f}": (lambda env, t, j=j: float(env.vec.scenario.init[0, t, j]),)
            for j, f in enumerate(POSE_FIELDS)},
     }
@@ -424,8 +428,8 @@ class ShipAssetsView(_View):
         "stop_flag": (lambda env, t: bool(env._state()["stop"][t, 0]),
                       lambda env, t, v: env._write("stop", t, int(bool(v)))),
         "type_tag": (lambda env, t: ("test_ship", "obs_ship")[t],),
-        "integrator_term": (lambda env, t: env._integrator_term[t],),
-        "time_list": (lambda env, t: env._time_list[t],),
+        "integrator_term": (lambda env, t: (env._flush(), env._integrator_term[t])[1],),
+        "time_list": (lambda env, t: (env._flush(), env._time_list[t])[1],),
     }
 
 
@@ -473,6 +477,25 @@ class MultiShipRLEnv:
         self.ship_draw = bool(ship_draw)
         self.time_since_last_ship_drawing = time_since_last_ship_drawing
         self.record = bool(record)
+        # per-step host arrays of sit_step_host (one ctypes call per step: the library stages the inputs
+        # in pinned coherent memory the kernel reads and writes directly, launches, copies the state
+        # blob when recording, synchronises once)
+        rs = 8 if precision == 64 else 4
+        self._rs, self._np_real = rs, (np.float64 if precision == 64 else np.float32)
+        self._act = np.zeros(2, self._np_real)
+        self._sac, self._init = np.zeros(1, np.uint8), np.zeros(1, np.uint8)
+        self._ns, self._rw = np.zeros(10, self._np_real), np.zeros(1, self._np_real)
+        self._dn, self._st = np.zeros(1, np.uint8), np.zeros(1, np.uint32)
+        self._log = np.zeros(_lib.SIT_LOG_ROWS, self._np_real)
+        # the state blob after a step (recording envs: every step; else fetched when a view reads it) and
+        # numpy views of it made once (building views per step cost ~0.15 ms of torch view calls)
+        self._blob_t = torch.zeros(self.vec._state_bytes, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+        self._host_state = {k: v.numpy() for k, v in self.vec._views(self._blob_t).items()}
+        ptr = lambda a: c_void_p(a.ctypes.data)  # noqa: E731
+        self._step_args = (self.vec.handle, ptr(self._act), ptr(self._sac), ptr(self._init), ptr(self._ns),
+                           ptr(self._rw), ptr(self._dn), ptr(self._st), ptr(self._log) if self.record else None,
+                           c_void_p(self._blob_t.data_ptr()) if self.record else None, self.vec._stream())
+        self._step_fn = self.vec.lib.sit_step_host
         r = scenario.routes[0, 1]
         nw = int(scenario.n_wpt[0, 1])
         self.observation_space = _Box(
@@ -497,34 +520,7 @@ class MultiShipRLEnv:
         self.assets = [self.test, self.obs]
         self._sim_results = [{}, {}]
         self._integrator_term, self._time_list = [[], []], [[], []]
-        # per-step staging: inputs [action (2 reals) | sac u8 | init u8]; outputs [next_state (10 reals) |
-        # reward | pad | action_out (4 reals) | log (62 reals) | status u32 | done u8]
-        rs = 8 if precision == 64 else 4
-        self._rs, self._np_real = rs, (np.float64 if precision == 64 else np.float32)
-        dev = self.vec.device
-        self._in_host = torch.zeros(2 * rs + 2, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
-        self._in_dev = torch.zeros(2 * rs + 2, dtype=torch.uint8, device=dev)
-        self._o_ns, self._o_rw, self._o_ao, self._o_lg = 0, 10 * rs, 12 * rs, 16 * rs
-        self._o_st = (16 + _lib.SIT_LOG_ROWS) * rs
-        self._o_dn = self._o_st + 4
-        # the post-step state blob follows the outputs: one device->host copy per step brings both, and
-        # the views read that copy
-        self._o_blob = (self._o_dn + 4 + 255) // 256 * 256
-        nbytes = self._o_blob + self.vec._state_bytes
-        self._out_dev = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
-        self._out_host = torch.zeros(nbytes, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
-        # numpy views of the state part of the host copy, made once: every step's copy lands in the same
-        # pinned buffer (building the views per step cost ~0.15 ms of torch view calls)
-        self._host_state = {k: v.numpy() for k, v in self.vec._views(self._out_host[self._o_blob:]).items()}
-        self._in_np, self._out_np = self._in_host.numpy(), self._out_host.numpy()
-        ra = _lib.RolloutArgs()
-        bi, bo = self._in_dev.data_ptr(), self._out_dev.data_ptr()
-        ra.n_steps, ra.auto_reset, ra.seed, ra.env_id_offset = 1, 0, 0, 0
-        ra.action_ne, ra.sac_update, ra.init = bi, bi + 2 * rs, bi + 2 * rs + 1
-        ra.next_state, ra.reward, ra.action_out = bo + self._o_ns, bo + self._o_rw, bo + self._o_ao
-        ra.status, ra.done = bo + self._o_st, bo + self._o_dn
-        ra.log = (bo + self._o_lg) if self.record else None
-        self._ra = ra
+        self._rows, self._n_flushed = [], 0
 
     # ---------------- reference methods ----------------
     def reward_function_params(self):
@@ -560,6 +556,7 @@ class MultiShipRLEnv:
         self.state = self.initial_state
         self._sim_results = [{}, {}]
         self._integrator_term, self._time_list = [[], []], [[], []]
+        self._rows, self._n_flushed = [], 0
         self._obs_stop_pre = False
         self.reward_function_params()
         return self.initial_state.copy()
@@ -572,25 +569,19 @@ class MultiShipRLEnv:
     def step(self, converted_action, SAC_update, init):
         """MultiShipRLEnv.step (MSRL_Env.py:404-442): returns (next_state list of 10 float,
         reward float, done bool, status str)."""
-        rs = self._rs
-        inp = self._in_np
-        inp[:2 * rs].view(self._np_real)[:] = (float(converted_action[0]), float(converted_action[1]))
-        inp[2 * rs] = 1 if SAC_update else 0
-        inp[2 * rs + 1] = 1 if init else 0
-        stream = self.vec._stream()
-        with torch.cuda.device(self.vec.device):
-            self._in_dev.copy_(self._in_host, non_blocking=True)
-            _lib.check(self.vec.lib.sit_rollout(self.vec.handle, self._ra, stream), self.vec.handle)
-            _lib.check(self.vec.lib.sit_get_state(self.vec.handle, self._out_dev.data_ptr() + self._o_blob, stream),
-                       self.vec.handle)
-            self._out_host.copy_(self._out_dev, non_blocking=True)
-            torch.cuda.current_stream(self.vec.device).synchronize()
-        self._cache = self._host_state
-        out = self._out_np
-        ns = out[:10 * rs].view(self._np_real)
-        reward = float(out[self._o_rw:self._o_rw + rs].view(self._np_real)[0])
-        status = int(out[self._o_st:self._o_st + 4].view(np.uint32)[0])
-        next_state = [float(x) for x in ns]
+        a = self._act
+        a[0] = converted_action[0]
+        a[1] = converted_action[1]
+        self._sac[0] = 1 if SAC_update else 0
+        self._init[0] = 1 if init else 0
+        rc = self._step_fn(*self._step_args)
+        if rc:
+            _lib.check(rc, self.vec.handle)
+        # recording envs have the post-step state on the host; otherwise a view fetches it on demand
+        self._cache = self._host_state if self.record else None
+        reward = float(self._rw[0])
+        status = int(self._st[0])
+        next_state = self._ns.tolist()
         if SAC_update:                                  # obs_step (MSRL_Env.py:326-340)
             self.prev_route_coordinate = (converted_action[0], converted_action[1])
         if self.ship_draw:                              # ship drawing timer (MSRL_Env.py:418-423; no drawing)
@@ -598,37 +589,50 @@ class MultiShipRLEnv:
                 self.time_since_last_ship_drawing = 0
             self.time_since_last_ship_drawing += self._dt
         if self.record:
-            self._record(out[self._o_lg:self._o_lg + _lib.SIT_LOG_ROWS * rs].view(self._np_real))
+            st = self._host_state
+            self._rows.append((self._log.copy(), float(st["e_ct_int"][0, 0]), float(st["e_ct_int"][1, 0]),
+                               self._obs_stop_pre))
+            self._obs_stop_pre = bool(st["stop"][1, 0])
         self.state = next_state
-        return next_state, reward, bool(out[self._o_dn]), status_string(status)
+        return next_state, reward, bool(self._dn[0]), _status_string(status)
 
-    def _record(self, row):
-        """simulation_results of both ships (store_simulation_data / store_last_simulation_data,
-        ship_model.py:645-700), reward_results running sums (MSRL_env_ex.py:926-964), and the assets'
-        integrator_term / time_list (MSRL_Env.py:264-265, 305-306, 374-375)."""
+    def _flush(self):
+        """The recorded steps not yet in the reference's containers: simulation_results of both ships
+        (store_simulation_data / store_last_simulation_data, ship_model.py:645-700), reward_results running
+        sums (MSRL_env_ex.py:926-964), and the assets' integrator_term / time_list (MSRL_Env.py:264-265,
+        305-306, 374-375).  Built when read, not on the step path."""
         nk = len(LOG_KEYS)
-        st = self._state()
-        for t in range(2):
-            res = self._sim_results[t]
-            for i, k in enumerate(LOG_KEYS):
-                res.setdefault(k, []).append(float(row[t * nk + i]))
-            self._integrator_term[t].append(float(st["e_ct_int"][t, 0]))
-            # the simulator time after the integration, before int.next_time(); a stopped obstacle ship
-            # appends it after the first of its two next_time() calls (MSRL_Env.py:293-309)
-            stop_path = t == 1 and self._obs_stop_pre
-            self._time_list[t].append(float(row[t * nk]) + (self._dt if stop_path else 0.0))
-        self._obs_stop_pre = bool(st["stop"][1, 0])
-        for j, (who, name) in enumerate(REWARD_SERIES):
-            lst = self.reward_results[who][name]
-            lst.append((lst[-1] if lst else 0) + float(row[2 * nk + j]))
+        for row, ect0, ect1, stop_pre in self._rows[self._n_flushed:]:
+            for t, ect in ((0, ect0), (1, ect1)):
+                res = self._sim_results[t]
+                for i, k in enumerate(LOG_KEYS):
+                    res.setdefault(k, []).append(float(row[t * nk + i]))
+                self._integrator_term[t].append(ect)
+                # the simulator time after the integration, before int.next_time(); a stopped obstacle ship
+                # appends it after the first of its two next_time() calls (MSRL_Env.py:293-309)
+                stop_path = t == 1 and stop_pre
+                self._time_list[t].append(float(row[t * nk]) + (self._dt if stop_path else 0.0))
+            for j, (who, name) in enumerate(REWARD_SERIES):
+                lst = self._reward_results[who][name]
+                lst.append((lst[-1] if lst else 0) + float(row[2 * nk + j]))
+        self._n_flushed = len(self._rows)
+
+    @property
+    def reward_results(self):
+        self._flush()
+        return self._reward_results
+
+    @reward_results.setter
+    def reward_results(self, v):
+        self._reward_results = v
 
     # ---------------- state access ----------------
     def _state(self):
-        """The env's device state as numpy arrays (one device->host copy of the state blob per step,
-        then cached)."""
+        """The env's device state as numpy arrays (the state blob, copied to the host once per step
+        when the env records, else when a view first reads it after a step; then cached)."""
         if self._cache is None:
-            blob = self.vec.state_blob().cpu()
-            self._cache = {k: v.numpy() for k, v in self.vec._views(blob).items()}
+            self._blob_t.copy_(self.vec.state_blob())
+            self._cache = self._host_state
         return self._cache
 
     def _write(self, field, t, value):

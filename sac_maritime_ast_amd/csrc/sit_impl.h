@@ -153,11 +153,18 @@ struct KArgs {
   StepIO<T> io;
   int32_t n_env;
   int32_t cap;
-  int32_t map_bytes;
+  int32_t map_bytes;   // bytes of the map blob staged into LDS (map_stage_bytes)
 };
 
-// Copy the edge records, the packed index and the class grid (the first map_bytes of the map
-// blob) into LDS at `dst`.
+// SIT_LDS_CELLS: the mixed-cell crossing records (frank, crec, clive: ~26 KB of the reference map's 57)
+// staged into LDS with the rest (1), or read through the caches (0: they are read only for points in
+// a mixed class cell, near a shore; the LDS block then holds edges, nearest-edge index and class grid)
+#ifndef SIT_LDS_CELLS
+#define SIT_LDS_CELLS 1
+#endif
+
+// Copy the edge records, the packed index and the class grid (and with SIT_LDS_CELLS the mixed-cell
+// records: the first map_bytes of the map blob) into LDS at `dst`.
 template <typename T>
 __device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* dst) {
   const unsigned char* src = reinterpret_cast<const unsigned char*>(a.map.edge);
@@ -174,9 +181,11 @@ __device__ __forceinline__ Map<T> stage_map(const KArgs<T>& a, unsigned char* ds
   m.edge = reinterpret_cast<const Edge<T>*>(dst);
   m.idx = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.idx) - src));
   m.fine = reinterpret_cast<const uint32_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.fine) - src));
+#if SIT_LDS_CELLS
   m.frank = reinterpret_cast<const uint16_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.frank) - src));
   m.crec = reinterpret_cast<const uint2*>(dst + (reinterpret_cast<const unsigned char*>(a.map.crec) - src));
   m.clive = reinterpret_cast<const uint8_t*>(dst + (reinterpret_cast<const unsigned char*>(a.map.clive) - src));
+#endif
   return m;
 }
 
@@ -1189,6 +1198,8 @@ struct sit_handle {
   double fx0 = 0, fy0 = 0, finvx = 0, finvy = 0;
   double min_n = 0, max_n = 0, min_e = 0, max_e = 0;
   bool have_map = false, have_routes = false, have_init = false;
+  unsigned char* stage = nullptr;       // sit_step_host: pinned coherent host staging
+  unsigned char* stage_dev = nullptr;   // its device address
 };
 
 namespace {
@@ -1362,6 +1373,9 @@ Consts<T> make_consts(const sit_handle* h) {
   return c;
 }
 
+// bytes of the map blob the fused step kernels stage into LDS (SIT_LDS_CELLS)
+size_t map_stage_bytes(const sit_handle* h) { return SIT_LDS_CELLS ? h->map_bytes : h->map_frank; }
+
 template <typename T>
 KArgs<T> make_args(const sit_handle* h) {
   KArgs<T> a{};
@@ -1404,7 +1418,7 @@ KArgs<T> make_args(const sit_handle* h) {
   a.map.n_live = (int32_t)h->n_live;
   a.map.off = reinterpret_cast<const int32_t*>(h->map + h->map_off);
   a.map.bbox = reinterpret_cast<const T*>(h->map + h->map_bbox);
-  a.map_bytes = (int32_t)h->map_bytes;
+  a.map_bytes = (int32_t)map_stage_bytes(h);
   return a;
 }
 
@@ -1429,7 +1443,7 @@ constexpr size_t kLdsCu = 160 * 1024;       // the CU's LDS (k_env_steps_sync: t
 #define SIT_LDS_MIN_STEPS 8
 #endif
 constexpr int kLdsMinSteps = SIT_LDS_MIN_STEPS;
-size_t map_lds_bytes(const sit_handle* h) { return (h->map_bytes + 255) & ~size_t(255); }
+size_t map_lds_bytes(const sit_handle* h) { return (map_stage_bytes(h) + 255) & ~size_t(255); }
 
 // the step kernel of a launch as a readable instantiation name (sit_step_kernel)
 template <typename T>
@@ -1454,7 +1468,7 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   // logged launches, and every launch under SIT_STEP_KERNEL=classic.  The sync kernel stages the map
   // into LDS for fused launches; single-step launches read it through the caches.
   const bool sync_lds = h->lds_map_sel == 1 || (h->lds_map_sel < 0 && io.n_steps >= kLdsMinSteps);
-  const size_t lds_sync = sync_lds ? sync_lds_bytes<T>(h->map_bytes) : sync_lds_bytes<T>(0);
+  const size_t lds_sync = sync_lds ? sync_lds_bytes<T>(map_stage_bytes(h)) : sync_lds_bytes<T>(0);
   if (!h->kernel_classic && !io.log && h->use_index && lds_sync + sizeof(Consts<T>) + 256 <= kLdsCu) {
     const void* kern = nullptr;
     auto pick = [&](auto mode_tag, auto mach_tag, auto lds_tag) {

@@ -286,6 +286,9 @@ void sit_destroy(sit_handle* h) {
   if (h->blob) (void)setup_free(h->blob);
   if (h->scen) (void)setup_free(h->scen);
   if (h->map) (void)setup_free(h->map);
+#ifndef SIT_HOST_MEMORY_TEST
+  if (h->stage) (void)hipHostFree(h->stage);
+#endif
   delete h;
 }
 
@@ -704,6 +707,77 @@ int sit_step(sit_handle* h, const void* action_ne, const uint8_t* sac_update, co
   return launch_steps_f32(h, io, stream);
 }
 
+// sit_step_host's staging: pinned, coherent host memory mapped for the device (the step kernel reads
+// the inputs and writes the outputs there directly; no copy call per step)
+struct StageLayout {
+  size_t act, sac, init, ns, rw, dn, st, log, blob, bytes;
+};
+static StageLayout stage_layout(const sit_handle* h) {
+  const size_t n = (size_t)h->n_env, rs = real_size(h);
+  StageLayout L{};
+  size_t o = 0;
+  L.act = o; o = align256(o + 2 * n * rs);
+  L.sac = o; o = align256(o + n);
+  L.init = o; o = align256(o + n);
+  L.ns = o; o = align256(o + (size_t)SIT_OBS_DIM * n * rs);
+  L.rw = o; o = align256(o + n * rs);
+  L.dn = o; o = align256(o + n);
+  L.st = o; o = align256(o + 4 * n);
+  L.log = o; o = align256(o + (size_t)SIT_LOG_ROWS * n * rs);
+  L.blob = o; o = align256(o + h->blob_bytes);
+  L.bytes = o;
+  return L;
+}
+
+int sit_step_host(sit_handle* h, const void* action_ne, const uint8_t* sac_update, const uint8_t* init,
+                  void* next_state, void* reward, uint8_t* done, uint32_t* status, void* log, void* state,
+                  void* stream) {
+  int rc = ready(h);
+  if (rc) return rc;
+  if (!action_ne || !sac_update || !init) return fail(h, SIT_E_INVALID, "action_ne, sac_update and init are required");
+#ifdef SIT_HOST_MEMORY_TEST
+  (void)next_state; (void)reward; (void)done; (void)status; (void)log; (void)state; (void)stream;
+  return fail(h, SIT_E_STATE, "sit_step_host: no device in the host-memory test build");
+#else
+  const StageLayout L = stage_layout(h);
+  if (!h->stage) {
+    HIP_TRY(h, hipHostMalloc(reinterpret_cast<void**>(&h->stage), L.bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    void* dp = nullptr;
+    HIP_TRY(h, hipHostGetDevicePointer(&dp, h->stage, 0));
+    h->stage_dev = static_cast<unsigned char*>(dp);
+  }
+  const size_t n = (size_t)h->n_env, rs = real_size(h);
+  std::memcpy(h->stage + L.act, action_ne, 2 * n * rs);
+  std::memcpy(h->stage + L.sac, sac_update, n);
+  std::memcpy(h->stage + L.init, init, n);
+  unsigned char* d = h->stage_dev;
+  hipStream_t s = (hipStream_t)stream;
+  if (h->precision == SIT_F64) {
+    StepIO<double> io{};
+    io.n_steps = 1; io.action_ne = (const double*)(d + L.act); io.sac_update = d + L.sac; io.init = d + L.init;
+    io.next_state = (double*)(d + L.ns); io.reward = (double*)(d + L.rw); io.done = d + L.dn;
+    io.status = (uint32_t*)(d + L.st); io.log = log ? (double*)(d + L.log) : nullptr;
+    rc = launch_steps<double>(h, io, s);
+  } else {
+    StepIO<float> io{};
+    io.n_steps = 1; io.action_ne = (const float*)(d + L.act); io.sac_update = d + L.sac; io.init = d + L.init;
+    io.next_state = (float*)(d + L.ns); io.reward = (float*)(d + L.rw); io.done = d + L.dn;
+    io.status = (uint32_t*)(d + L.st); io.log = log ? (float*)(d + L.log) : nullptr;
+    rc = launch_steps_f32(h, io, stream);
+  }
+  if (rc) return rc;
+  if (state) HIP_TRY(h, hipMemcpyAsync(h->stage + L.blob, h->blob, h->blob_bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(h, hipStreamSynchronize(s));
+  if (next_state) std::memcpy(next_state, h->stage + L.ns, (size_t)SIT_OBS_DIM * n * rs);
+  if (reward) std::memcpy(reward, h->stage + L.rw, n * rs);
+  if (done) std::memcpy(done, h->stage + L.dn, n);
+  if (status) std::memcpy(status, h->stage + L.st, 4 * n);
+  if (log) std::memcpy(log, h->stage + L.log, (size_t)SIT_LOG_ROWS * n * rs);
+  if (state) std::memcpy(state, h->stage + L.blob, h->blob_bytes);
+  return SIT_OK;
+#endif
+}
+
 int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
   int rc = ready(h);
   if (rc) return rc;
@@ -782,6 +856,9 @@ int sit_get_state(sit_handle* h, void* dst, void* stream) {
 int sit_set_state(sit_handle* h, const void* src, void* stream) {
   if (!h || !src) return fail(h, SIT_E_INVALID, "null argument");
   HIP_TRY(h, hipMemcpyAsync(h->blob, src, h->blob_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  // the cached IW terrain tests (iw_key_*) are answers for the map of the handle that saved the blob:
+  // a restored state re-tests its IW against this handle's map
+  HIP_TRY(h, hipMemsetAsync(h->blob + h->off[F_IWK_FLAGS], 0, (size_t)h->n_env * 4, (hipStream_t)stream));
   return SIT_OK;
 }
 

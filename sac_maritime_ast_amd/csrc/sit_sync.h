@@ -665,8 +665,18 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
 
 // LDSMAP: the island map staged into LDS per block (fused launches) or read through the caches
 // (single-step launches, whose prologue cannot amortise staging 57 KB per block)
+// SIT_SYNC_WAVES_PER_EU: the occupancy the kernel's registers are allocated for (waves per SIMD; 0 = the
+// compiler's choice).  Three blocks per CU need <= 168 VGPRs and <= 53 KB of LDS per block
+#ifndef SIT_SYNC_WAVES_PER_EU
+#define SIT_SYNC_WAVES_PER_EU 0
+#endif
+#if SIT_SYNC_WAVES_PER_EU > 0
+#define SIT_SYNC_OCC __attribute__((amdgpu_waves_per_eu(SIT_SYNC_WAVES_PER_EU, SIT_SYNC_WAVES_PER_EU)))
+#else
+#define SIT_SYNC_OCC
+#endif
 template <typename T, int MODE, int MACH, bool LDSMAP>
-__global__ __launch_bounds__(256) void k_env_steps_sync(const KArgs<T> a) {
+__global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Consts<T> cs;
   for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)

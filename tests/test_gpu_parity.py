@@ -750,3 +750,88 @@ def test_launch_partition_invariance(precision, kernel, monkeypatch):
             assert np.array_equal(sa[q], sb[q]), q
     iw = int(((a["status"] & _lib.ST_OBS_IW_TERMINAL) != 0).sum())
     print(f"launch partition f{precision} {kernel}: {iw} IW terminations, identical")
+
+
+def test_state_restore_across_maps_retests_iw():
+    """A state blob saved on one map and restored on a handle with another map: the restored handle
+    re-tests the IW against its own map (sit_set_state clears the single-step IW-test cache,
+    iw_key_*) instead of reusing the other map's answer.  The IW lies in open water on the reference
+    map and inside an extra island on the second map."""
+    n_env = 64
+    sc = make_scenario(n_env, cap=32)
+    obs_n, obs_e = sc.init[:, 1, 0], sc.init[:, 1, 1]
+    iw = np.stack([obs_n + 400.0, obs_e], 1)           # 400 m north of the obstacle's start: open water
+    c_n, c_e = float(iw[:, 0].mean()), float(iw[:, 1].mean())
+    half = 150.0 + float(np.ptp(iw[:, 0]) + np.ptp(iw[:, 1]))
+    island = np.array([[c_e - half, c_n - half], [c_e + half, c_n - half], [c_e + half, c_n + half],
+                       [c_e - half, c_n + half]])        # (east, north) vertices around every IW
+    sc_b = Scenario(sc.routes, sc.n_wpt, sc.init, list(sc.polys) + [island])
+    outs = []
+    for scen in (sc, sc_b):
+        e = VecMultiShipRLEnv(scenario=scen, precision=64, device=DEV)
+        e.reset()
+        e.init_step()
+        outs.append(e)
+    a, b = outs
+    ones, zeros = np.ones(n_env, np.uint8), np.zeros(n_env, np.uint8)
+    _, _, _, st0 = a.step(iw, ones, ones)
+    _, _, _, st1 = a.step(iw, zeros, zeros)
+    assert not ((st0 | st1) & _lib.ST_OBS_IW_TERMINAL).any(), "the IW should be in open water on map A"
+    assert (np_state(a)["iw_key_flags"] & 1).all(), "map A's IW test was not cached"
+    b.load_state_blob(a.state_blob())
+    _, _, _, st2 = b.step(iw, zeros, zeros)
+    assert ((st2 & _lib.ST_OBS_IW_TERMINAL) != 0).all(), "the restored handle reused map A's IW test"
+
+
+@pytest.mark.parametrize("steps", [1, 16])
+@pytest.mark.parametrize("precision", [64, 32])
+def test_sync_kernel_equals_classic_explicit_no_reset(precision, steps, monkeypatch):
+    """Explicit actions without auto-reset (the drop-in's sit_step / rollout(actions=...)): the two-wave
+    kernel against k_env_steps from the same desynchronised state, over 2000 envs and 96 steps in
+    launches of `steps` (1: the map read through the caches with the IW-test cache; 16: the LDS map).
+    IWs near the obstacle ship, inserted at random steps (1 %), many into terrain.  Final stop flags,
+    next waypoint and route length identical; outputs within 1e-9 (f64) / 1e-5 (f32) against the
+    per-field floors, done and status identical."""
+    n_env, total = 2000, 96
+    base = VecMultiShipRLEnv(scenario=make_scenario(n_env, cap=48), precision=precision, device=DEV)
+    base.reset()
+    base.init_step()
+    base.rollout(600, seed=40)
+    blob = base.state_blob()
+    st = np_state(base)
+    rng = np.random.default_rng(5)
+    ang = rng.uniform(-np.pi, np.pi, (total, n_env))
+    dist = rng.uniform(200.0, 1500.0, (total, n_env))
+    act = np.stack([st["north"][1] + dist * np.cos(ang), st["east"][1] + dist * np.sin(ang)], -1)
+    sac = (rng.random((total, n_env)) < 0.01).astype(np.uint8)
+    init = np.zeros((total, n_env), np.uint8)
+    res = {}
+    for kernel in ("classic", "sync"):
+        if kernel == "classic":
+            monkeypatch.setenv("SIT_STEP_KERNEL", "classic")
+        env = VecMultiShipRLEnv(scenario=base.scenario, precision=precision, device=DEV)
+        monkeypatch.delenv("SIT_STEP_KERNEL", raising=False)
+        env.load_state_blob(blob)
+        rows = {q: [] for q in ("next_state", "reward", "done", "status")}
+        for k0 in range(0, total, steps):
+            sl = slice(k0, k0 + steps)
+            o = env.rollout(steps, auto_reset=False, actions={"action_ne": act[sl], "sac_update": sac[sl],
+                                                              "init": init[sl]}, transition_capacity=0)
+            for q in rows:
+                rows[q].append(o[q].cpu().numpy())
+        name = env.lib.sit_step_kernel(env.handle).decode()
+        assert name.startswith("k_env_steps_sync<" if kernel == "sync" else "k_env_steps<"), name
+        assert ("map=global" in name) == (steps == 1), name
+        res[kernel] = ({q: np.concatenate(v) for q, v in rows.items()}, np_state(env))
+    (x, sx), (y, sy) = res["classic"], res["sync"]
+    tol = TOL64 if precision == 64 else 1e-5
+    for q in ("done", "status"):
+        assert np.array_equal(x[q], y[q]), q
+    assert rel_err(y["next_state"], x["next_state"], OBS_SCALE).max() <= tol
+    assert np.abs(y["reward"] - x["reward"]).max() <= tol * max(1.0, float(np.abs(x["reward"]).max()))
+    for q in ("stop", "next_wpt", "n_wpt"):
+        assert np.array_equal(sx[q], sy[q]), q
+    n_iw = int(((x["status"] & _lib.ST_OBS_IW_TERMINAL) != 0).sum())
+    n_stop = int(sx["stop"].sum())
+    print(f"explicit no-reset f{precision} K={steps}: {n_iw} IW-terminal rows, {n_stop} stopped ships")
+    assert n_iw > 0 and n_stop > 0

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Per-call latency of the scalar drop-in (compat.MultiShipRLEnv.step: one H2D copy, one kernel
-launch, one D2H copy, host bookkeeping) on the reference's nominal episode, built from the
-reference-form constructor (stand-ins of its ShipAssets, tests/ref_assets.py).  Writes one JSON line.
+"""Per-call latency of the scalar drop-in (compat.MultiShipRLEnv.step: one sit_step_host call -- the
+inputs staged in pinned coherent memory the kernel reads and writes directly, one launch, the state blob
+copied when recording, one synchronisation -- plus the host bookkeeping) on the reference's nominal
+episode, built from the reference-form constructor (stand-ins of its ShipAssets, tests/ref_assets.py).
+Writes one JSON line.
 The reference's own env step measured 0.86 ms (full two-ship MultiShipRLEnv.step with
 reward, one core)."""
 import json
@@ -26,14 +28,19 @@ def run(precision, record, n=600):
                          precision=precision, wpt_capacity=d["routes"].shape[1], record=record)
     env.reset()
     env.init_step()
+    # the recorded actions as plain Python values (an NpzFile re-reads and decompresses an array on
+    # every d[key] access: inside the timed call that was most of round 3's 173 us)
+    acts = [(float(a), float(b)) for a, b in zip(d["action_n"][:n], d["action_e"][:n])]
+    sacs, inits = [bool(x) for x in d["sac_update"][:n]], [bool(x) for x in d["init"][:n]]
     lat = []
     for i in range(n):
-        a = (float(d["action_n"][i]), float(d["action_e"][i]))
+        a, sac, ini = acts[i], sacs[i], inits[i]
         t0 = time.perf_counter()
-        env.step(a, bool(d["sac_update"][i]), bool(d["init"][i]))
+        env.step(a, sac, ini)
         lat.append(time.perf_counter() - t0)
     v = np.asarray(lat[50:]) * 1e6
-    return {"precision": precision, "record": record, "steps": len(v), "median_us": float(np.median(v)),
+    kernel = env.vec.lib.sit_step_kernel(env.vec.handle).decode()
+    return {"precision": precision, "record": record, "kernel": kernel, "steps": len(v), "median_us": float(np.median(v)),
             "p10_us": float(np.percentile(v, 10)), "p90_us": float(np.percentile(v, 90)),
             "mean_us": float(v.mean())}
 

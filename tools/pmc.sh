@@ -1,7 +1,9 @@
 #!/bin/bash
 # PMC passes for the step kernel, one rocprofv3 run per counter group (gfx950 slot limits).
 set -u
-out=gpurun_out/pmc
+# usage: tools/pmc.sh <out dir> [bench.py args...]
+out=$1
+shift
 mkdir -p $out
 BENCH="python3 bench.py --no-cpu-baseline $*"
 i=0
