@@ -492,10 +492,28 @@ def test_f32_free_running_within_storage_bound():
     outcome differs (done, status, sampling event, waypoint index, route length, stop flags, episode
     step, sampler counter).  Gated: before divergence the next_state deviation (per-field floors) is
     within SURVEY §8(d)'s storage bound 2.5e-5; the float32 arithmetic adds at most 50 % to what
-    storage alone costs; at most 2 % of envs diverge (a decision moved by float32 state drift)."""
+    storage alone costs; at most 2 % of envs diverge.  Every divergence is attributed
+    (f32_drift.measure(attribute=True)): re-run in float64 from the float32 run's own pre-step state,
+    the step takes the float32 decision (the state's float32 drift decided it), or, where it takes the
+    float64 one, the flip is a hull-in-terrain decision whose exact (float64) predicate at the stored
+    float32 post-step position IS the float32 decision, with a hull corner closer to the shore than the
+    two runs' positions differ (the float32 rounding of the position moved it, not the predicate's
+    arithmetic)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import f32_drift
-    rep = f32_drift.measure(4096, 2000, 77, log=False)
+    rep = f32_drift.measure(4096, 2000, 77, log=False, attribute=True)
+    att = rep["f32_flip_attribution"]
+    assert att["envs"] == rep["f32"]["envs_diverged"] and att["neither"] == 0
+    for f in att["flips"]:
+        if f["exact_from_f32_state_takes"] == "f32 decision":
+            continue
+        assert f["hull"], f"env {f['env']} step {f['step']}: float32 arithmetic flipped {f['flipped']}"
+        t = 1 if (f["status_bits_f32"] ^ f["status_bits_f64"]) & _lib.ST_OBS_TERRAIN else 0
+        h = f["hull"][f"ship{t}"]
+        got32 = bool(f["status_bits_f32"] & (_lib.ST_OBS_TERRAIN if t else _lib.ST_TEST_TERRAIN))
+        assert h["hull_in_terrain_exact_at_f32_position"] == got32, f"env {f['env']}: hull predicate"
+        assert min(h["min_corner_boundary_distance_m_f32"], h["min_corner_boundary_distance_m_f64"]) \
+            <= h["position_difference_m"], f"env {f['env']}: not a position knife edge"
     f32, s32 = rep["f32"], rep["s32"]
     print(f"f32 vs f64 free-running: {f32['envs_diverged']} envs diverged (earliest step "
           f"{f32['earliest_divergence_step']}), next_state max {f32['next_state_max']:.2e} p99 "

@@ -41,8 +41,31 @@ def rel(a, b, floor):
     return np.abs(a.astype(np.float64) - b.astype(np.float64)) / np.maximum(np.abs(b.astype(np.float64)), floor)
 
 
-def measure(n_env=4096, steps=2000, seed=77, log=True):
-    """The report (a dict) of n_env envs x steps steps; tests/test_gpu_parity.py gates on it."""
+def _discrete(o, st):
+    """The discrete outcome of a step per env: done, status, sampling event, state integers."""
+    d = {"done": o["done"], "status": o["status"], "sac": o["sac"]}
+    for f in INTS:
+        d[f] = st[f]
+    return d
+
+
+def _differs(a, b):
+    """Per env: which discrete quantities differ (list of names per env)."""
+    n = a["done"].shape[-1]
+    out = [[] for _ in range(n)]
+    for k in a:
+        d = a[k] != b[k]
+        d = d.any(0) if d.ndim == 2 else d
+        for e in np.nonzero(d)[0]:
+            out[e].append(k)
+    return out
+
+
+def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False):
+    """The report (a dict) of n_env envs x steps steps; tests/test_gpu_parity.py gates on it.
+    attribute: for every env at its first float32 divergence, re-run that step in float64 from the
+    float32 run's own pre-step state (a float64 handle of the same envs and global ids, teacher-forced
+    for one step) and record which of the two decisions the exact arithmetic takes there."""
     args = argparse.Namespace(n_env=n_env, steps=steps, seed=seed)
     n = args.n_env
     sc = make_scenario(n, cap=48)
@@ -55,12 +78,63 @@ def measure(n_env=4096, steps=2000, seed=77, log=True):
     ns_dev = {k: np.zeros((n, 10)) for k in first}
     st_dev = {k: {f: np.zeros((2, n)) for f in REAL} for k in first}
     outs = {k: {} for k in envs}
+    flips = []
+    tf = VecMultiShipRLEnv(scenario=sc, precision=64, device="cuda:0") if attribute else None
     for step in range(args.steps):
         res = {}
+        pre = {k: state(envs[k]) for k in ("f32", "f64")} if attribute else None
         for k, e in envs.items():
             o = e.rollout(1, seed=args.seed, out=outs[k])
             res[k] = ({q: o[q][0].cpu().numpy() for q in ("next_state", "reward", "done", "status")} |
                       {"sac": o["action"][0, :, 3].cpu().numpy()}, state(e))
+        if attribute:
+            d32, d64 = _discrete(*res["f32"]), _discrete(*res["f64"])
+            w32 = _differs(d32, d64)
+            new_div = [e for e, w in enumerate(w32) if w and first["f32"][e] == args.steps]
+            if new_div:
+                # the float64 kernel, one step from the float32 run's pre-step state (every env; the
+                # sampler draws are keyed by (seed, global env id, event), so they are the same draws)
+                tf.set_state({f: v.astype(np.float64) if v.dtype == np.float32 else v for f, v in pre["f32"].items()})
+                o = tf.rollout(1, seed=args.seed)
+                dtf = _discrete({q: o[q][0].cpu().numpy() for q in ("done", "status")} |
+                                {"sac": o["action"][0, :, 3].cpu().numpy()}, state(tf))
+                wtf32, wtf64 = _differs(dtf, d32), _differs(dtf, d64)
+                # post-step positions before any auto reset: the next_state rows (test n, e at 0, 1;
+                # obstacle n, e at 6, 7)
+                ns32, ns64 = res["f32"][0]["next_state"], res["f64"][0]["next_state"]
+                for e in new_div:
+                    # status flips are terrain / hull predicates of the post-step position: the exact
+                    # (float64, GEOS-restated) hull and corner distances at the float32 run's and at the
+                    # float64 run's post-step positions (sit_probe_map on the float64 handle)
+                    hull = {}
+                    if d32["status"][e] != d64["status"][e]:
+                        half = 0.5 * float(envs["f64"].params.length_of_ship)
+                        for t in (0, 1):
+                            pts = []
+                            for src in (ns32, ns64):
+                                n0, e0 = float(src[e, 6 * t]), float(src[e, 6 * t + 1])
+                                pts += [[n0, e0]] + [[n0 + a * half, e0 + b * half] for a in (-1, 1) for b in (-1, 1)]
+                            dist, _, hl = tf.probe_map(np.asarray(pts))
+                            dist, hl = dist.cpu().numpy(), hl.cpu().numpy()
+                            hull[f"ship{t}"] = {
+                                "hull_in_terrain_exact_at_f32_position": bool(hl[0]),
+                                "hull_in_terrain_exact_at_f64_position": bool(hl[5]),
+                                "min_corner_boundary_distance_m_f32": float(dist[1:5].min()),
+                                "min_corner_boundary_distance_m_f64": float(dist[6:10].min()),
+                                "position_difference_m": float(np.hypot(ns32[e, 6 * t] - ns64[e, 6 * t],
+                                                                        ns32[e, 6 * t + 1] - ns64[e, 6 * t + 1]))}
+                    flips.append({
+                        "env": int(e), "step": int(step), "flipped": w32[e],
+                        "exact_from_f32_state_takes": ("f32 decision" if not wtf32[e] else
+                                                       "f64 decision" if not wtf64[e] else "neither"),
+                        "status_bits_f32": int(d32["status"][e]), "status_bits_f64": int(d64["status"][e]),
+                        "next_wpt_f32": [int(x) for x in d32["next_wpt"][:, e]],
+                        "next_wpt_f64": [int(x) for x in d64["next_wpt"][:, e]],
+                        # how far the float32 run's state had drifted from the float64 run's before the step
+                        "pre_state_rel_dev_max": float(max(rel(pre["f32"][f][:, e], pre["f64"][f][:, e],
+                                                               SCALE[f]).max() for f in REAL)),
+                        "hull": hull,
+                    })
         # s32: float32 state storage (every real field of the state rounded after the step)
         s = res["s32"][1]
         envs["s32"].set_state({f: v.astype(np.float32).astype(np.float64) for f, v in s.items()
@@ -96,6 +170,20 @@ def measure(n_env=4096, steps=2000, seed=77, log=True):
              "state_per_field_max": {f"{f}[{s}]": float(st_dev[k][f][s].max()) for f in REAL for s in (0, 1)},
              "argmax_env": int(ns_dev[k].max(1).argmax())}
         report[k] = r
+    if attribute:
+        for f in flips:
+            f["storage_only_run_diverges_at"] = int(first["s32"][f["env"]]) if first["s32"][f["env"]] < args.steps else None
+        takes = [f["exact_from_f32_state_takes"] for f in flips]
+        report["f32_flip_attribution"] = {
+            "how": "for every env at its first float32 divergence (step t): the float64 kernel re-runs step t "
+                   "from the float32 run's own pre-step state (same envs, global ids and sampler draws). "
+                   "'f32 decision': exact arithmetic from the drifted state decides as the float32 step did, so "
+                   "the flip comes from the state's accumulated float32 rounding (storage), not from the float32 "
+                   "arithmetic of that step; 'f64 decision': the float32 arithmetic of the step flipped it.",
+            "envs": len(flips), "exact_takes_f32_decision": takes.count("f32 decision"),
+            "exact_takes_f64_decision": takes.count("f64 decision"), "neither": takes.count("neither"),
+            "also_diverge_in_storage_only_run": sum(1 for f in flips if f["storage_only_run_diverges_at"] is not None),
+            "flips": flips}
     return report
 
 
@@ -105,8 +193,9 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=77)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--attribute", action="store_true", help="attribute every float32 divergence (see measure)")
     args = ap.parse_args()
-    report = measure(args.n_env, args.steps, args.seed)
+    report = measure(args.n_env, args.steps, args.seed, attribute=args.attribute)
     txt = json.dumps(report, indent=1)
     print(txt)
     if args.out:
