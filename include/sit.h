@@ -340,7 +340,7 @@ typedef struct sit_rollout_args {
   /* sampling-event transitions (synthetic sampler mode): one record per step whose
    * SAC_update is set, appended at transition_count (atomic); records beyond
    * transition_capacity are counted but not written */
-  void* transitions;          /* real[transition_capacity][SIT_TRANSITION_DIM] or NULL */
+  void* transitions;          /* real[transition_capacity][SIT_TRANSITION_DIM] or NULL, 4-real aligned */
   int32_t* transition_count;  /* int32[1] */
   int32_t transition_capacity;
   int32_t mask_horizon;       /* args.num_steps_episode (main_ast.py:71, 387); 0 = none */

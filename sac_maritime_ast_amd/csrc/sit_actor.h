@@ -24,6 +24,10 @@ namespace {
 constexpr int kActorObs = SIT_OBS_DIM;
 constexpr int kActorHidden = SIT_ACTOR_HIDDEN;
 constexpr int kActorRows = 8;
+#ifndef SIT_ACTOR_KB
+#define SIT_ACTOR_KB 32   // W2^T float4 rows per prefetch batch and lane (2 batches in flight); 64 / KB batches
+#endif
+static_assert(64 % SIT_ACTOR_KB == 0 && SIT_ACTOR_KB % 4 == 0, "actor prefetch batch");
 // packed weights (float32): W1 [H][obs] (torch Linear layout), b1 [H], W2^T [H in][H out],
 // b2 [H], W3 [2][H], b3 [2]
 constexpr int kActorW1 = 0;
@@ -65,7 +69,7 @@ __global__ __launch_bounds__(256) void k_policy_actor(int cap, const float* __re
   const int q = j >> 6, l = j & 63;
   const float4* w2 = reinterpret_cast<const float4*>(w + kActorW2T) + l;
   const int kq = q * 64;
-  constexpr int KB = 32;                 // W2^T rows in flight per lane (two batches)
+  constexpr int KB = SIT_ACTOR_KB;       // W2^T rows in flight per lane (two batches)
   float4 wa[KB], wb[KB];
 #pragma unroll
   for (int i = 0; i < KB; ++i) wa[i] = w2[(kq + i) * (H / 4)];

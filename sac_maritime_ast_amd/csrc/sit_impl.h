@@ -414,6 +414,14 @@ __device__ void diag_wave(int type, int lane, bool act, const int* v) {
 // instructions per wave; the scattered row stride makes store issue, not bytes, the cost)
 __device__ __forceinline__ void store2(float* p, float a, float b) { *reinterpret_cast<float2*>(p) = make_float2(a, b); }
 __device__ __forceinline__ void store2(double* p, double a, double b) { *reinterpret_cast<double2*>(p) = make_double2(a, b); }
+// four reals at a 4-real-aligned address (replay-transition records: 24 reals = six of these)
+__device__ __forceinline__ void store4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void store4(double* p, double a, double b, double c, double d) {
+  store2(p, a, b);
+  store2(p + 2, c, d);
+}
 
 // IW = obstacle position + AB_len (cos, sin)(AB_alpha + a): float trig for the float handle
 // (1e-7 relative of AB_len, inside its 1e-5 contract), double for the float64 handle

@@ -791,6 +791,8 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     return fail(h, SIT_E_INVALID, "next_state and action_out must be aligned to 2 reals");
   if (ra->transitions && (!ra->transition_count || ra->transition_capacity <= 0))
     return fail(h, SIT_E_INVALID, "transitions need transition_count and a positive capacity");
+  if (reinterpret_cast<uintptr_t>(ra->transitions) % (4 * real_size(h)) != 0)
+    return fail(h, SIT_E_INVALID, "transitions must be aligned to 4 reals");
   if (ra->policy_action && ra->action_ne)
     return fail(h, SIT_E_INVALID, "policy mode and explicit actions are exclusive");
   if (ra->policy_action && (!ra->policy_ready || !ra->request_env || !ra->request_noise || !ra->request_obs ||

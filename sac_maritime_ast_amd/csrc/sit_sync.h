@@ -502,15 +502,16 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
           base = __shfl(base, lead);
           const int slot = base + (int)__popcll(m & ((1ull << lane) - 1ull));
           if (sac && slot < a.io.transition_capacity) {
+            // the 24-real record (include/sit.h) as six 4-real stores (a record starts 4-real aligned)
             T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
-            for (int q = 0; q < SIT_OBS_DIM; ++q) rec[q] = lo[q];
-            rec[10] = xd.o[4][lane];
-            rec[11] = reward;
-            for (int q = 0; q < 6; ++q) rec[12 + q] = nt[q];
-            for (int q = 0; q < 4; ++q) rec[18 + q] = no[q];
             const bool horizon_hit = (uf & kUfMaskH) && xd.ep[lane] + 2 == a.io.mask_horizon;
-            rec[22] = (horizon_hit || !env_done) ? T(1) : T(0);
-            rec[23] = (T)(a.io.env_id_offset + env);
+            const T mask = (horizon_hit || !env_done) ? T(1) : T(0);
+            store4(rec, lo[0], lo[1], lo[2], lo[3]);
+            store4(rec + 4, lo[4], lo[5], lo[6], lo[7]);
+            store4(rec + 8, lo[8], lo[9], xd.o[4][lane], reward);
+            store4(rec + 12, nt[0], nt[1], nt[2], nt[3]);
+            store4(rec + 16, nt[4], nt[5], no[0], no[1]);
+            store4(rec + 20, no[2], no[3], mask, (T)(a.io.env_id_offset + env));
           }
         }
       }

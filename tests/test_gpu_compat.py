@@ -255,3 +255,24 @@ def test_reference_constructor_float32_and_space_api():
     assert a.shape == (1,) and env.action_space.contains(a)
     assert env.observation_space.shape == (10,)
     assert env.ship_model.int.time == env.test.ship_model.int.time == 300 * 0.5
+
+
+@pytest.mark.parametrize("record", [True, False])
+def test_drop_in_step_kernel(record):
+    """Which step kernel the scalar drop-in runs (sit_step_kernel): a recording env (the default; its
+    step returns the trajectory-log row that builds simulation_results) runs the one-wave logged
+    k_env_steps; record=False runs the two-wave k_env_steps_sync with the map read through the caches
+    (DESIGN.md §4.1a).  Both through the one host-array call, sit_step_host."""
+    d = golden("env_nominal")
+    env = MultiShipRLEnv(fixture_assets(d), polygon_obstacle(), False, 30, ref_args(), device=DEV,
+                         wpt_capacity=d["routes"].shape[1], record=record)
+    env.reset()
+    env.init_step()
+    env.step((float(d["action_n"][0]), float(d["action_e"][0])), bool(d["sac_update"][0]), bool(d["init"][0]))
+    name = env.vec.lib.sit_step_kernel(env.vec.handle).decode()
+    if record:
+        assert name.startswith("k_env_steps<double,kExplicit,") and ",log," in name, name
+        assert len(env.test.ship_model.simulation_results["time [s]"]) == 1
+    else:
+        assert name.startswith("k_env_steps_sync<double,kExplicit,map=global"), name
+        assert env.test.ship_model.simulation_results == {}
