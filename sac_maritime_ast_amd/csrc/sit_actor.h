@@ -25,7 +25,8 @@ constexpr int kActorObs = SIT_OBS_DIM;
 constexpr int kActorHidden = SIT_ACTOR_HIDDEN;
 constexpr int kActorRows = 8;
 #ifndef SIT_ACTOR_KB
-#define SIT_ACTOR_KB 32   // W2^T float4 rows per prefetch batch and lane (2 batches in flight); 64 / KB batches
+#define SIT_ACTOR_KB 8    // W2^T float4 rows per prefetch batch and lane (2 batches in flight): 8 = 144 VGPRs, three
+                          // blocks per CU (C5 +2.6 % over 32: 188 VGPRs, two; 16: 168 VGPRs, +1.8 %)
 #endif
 static_assert(64 % SIT_ACTOR_KB == 0 && SIT_ACTOR_KB % 4 == 0, "actor prefetch batch");
 // packed weights (float32): W1 [H][obs] (torch Linear layout), b1 [H], W2^T [H in][H out],
@@ -356,6 +357,7 @@ __global__ __launch_bounds__(kAdmitThreads) void k_policy_admit(const KArgs<T> a
   const bool admit = waiting && (b > bcut || (b == bcut && rank < gcq));
   const int row = gbase + (int)__popcll(__ballot(admit) & lt);
   if (!admit) return;
+  // (loading every lane's observation before the plan, to overlap its latency, measured no faster)
   T v[SIT_OBS_DIM];
 #pragma unroll
   for (int k = 0; k < SIT_OBS_DIM; ++k) v[k] = a.st.last_obs[(size_t)k * n_env + e];
