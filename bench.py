@@ -66,7 +66,11 @@ def parse():
                     help="rollout: fused K-step launches (synthetic sampler); step: one sit_step launch "
                          "per env step; policy: Gaussian-policy actor between launches (config C5)")
     ap.add_argument("--groups", type=int, default=2, help="policy mode: env groups on separate streams")
-    ap.add_argument("--request-div", type=int, default=4, help="policy mode: request capacity = envs / this")
+    ap.add_argument("--request-div", type=int, default=4,
+                    help="policy mode, --serve queue: request capacity = envs / this")
+    ap.add_argument("--serve", choices=("kernel", "queue"), default="kernel",
+                    help="policy mode: the step kernel serves its waiting envs itself (default), or the request "
+                         "queue + sit_policy_actor between launches")
     ap.add_argument("--graph-launches", type=int, default=16, help="policy mode: launches per HIP graph")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-baseline-workers", type=int, default=16,
@@ -462,9 +466,10 @@ def bench_rollout(args, rank, world, dev):
 
 
 def bench_policy(args, rank, world, dev):
-    """Config C5: the SAC-AST Gaussian policy (fp32 actor, 256x256 MLP, one HIP kernel) chooses the
-    IWs; envs split into `--groups` groups on separate HIP streams so one group's actor runs while
-    the others' env kernels run.  value = env-steps executed (device counter) / time.  At N > 1
+    """Config C5: the SAC-AST Gaussian policy (fp32 actor, 256x256 MLP) chooses the IWs, evaluated by
+    the step kernel for its waiting envs at the end of each launch (--serve kernel), or between
+    launches on the request queue (--serve queue: sit_policy_actor); envs may be split into `--groups`
+    groups on separate HIP streams.  value = env-steps executed (device counter) / time.  At N > 1
     every group's replay transitions (all launches of a HIP graph append to one buffer) go to the
     learner (rank 0) over RCCL after each graph replay, pipelined behind the next replay."""
     from sac_maritime_ast_amd import VecMultiShipRLEnv, make_scenario
@@ -486,8 +491,9 @@ def bench_policy(args, rank, world, dev):
                                 precision=args.precision, device=dev)
         env.reset()
         env.init_step()
+        cap = None if args.serve == "kernel" else max(256, per // args.request_div)
         samplers.append(PolicySampler(env, policy, chunk=chunk, seed=args.seed, env_id_offset=off,
-                                      request_capacity=max(256, per // args.request_div), transition_capacity=tcap))
+                                      request_capacity=cap, transition_capacity=tcap, serve=args.serve))
     runner = OverlappedPolicySampler(samplers) if G > 1 else None
     cur = torch.cuda.current_stream(dev)
     # kernel duration of the env launches: eager launches through the sampler (HIP events on each
@@ -549,10 +555,12 @@ def bench_policy(args, rank, world, dev):
     rl["note"] = "per group launch (n_env / groups envs), groups run concurrently on separate streams"
     rl["kernel_ms_statistic"] = f"median over {n_ev * G} eager launches (HIP events on each group's stream)"
     cfg = {"workload": "C5: 65 536 ships driven by the SAC-AST Gaussian policy (256x256 MLP, fp32, "
-                       "fused into one HIP actor kernel) interleaved with the HIP env step on "
-                       "separate streams" if world == 1 else
+                       "evaluated in HIP for the envs waiting at each sampling event) and the HIP env step"
+                       if world == 1 else
                        f"C5 x{world}: {2 * n_env * world} policy-driven ships sharded over {world} GPUs",
-           "actor": "sit_policy_actor (fused)" if all(sm.fused for sm in samplers) else "PyTorch-ROCm",
+           "actor": ("in the step kernel (sit_rollout_args.actor_weights)" if args.serve == "kernel" else
+                     "sit_policy_actor (fused) on the request queue, capacity n/" + str(args.request_div))
+                    if all(sm.fused for sm in samplers) else "PyTorch-ROCm",
            "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env, "fused_steps_per_launch": chunk,
            "mode": "policy", "stream_groups": G, "launches_per_hip_graph": per_graph,
            "parallelism": f"env-shard x{world}",

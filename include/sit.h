@@ -377,6 +377,19 @@ typedef struct sit_rollout_args {
    * the fuel consumption accumulates over logged steps only (logging-only quantities). */
   void* log;
   int32_t* request_age;       /* int32[n_env] (policy mode): admission rounds waited, see above */
+  /* In-kernel serving (policy mode, optional).  With actor_weights != NULL the launch evaluates the
+   * actor itself — sit_policy_actor's network, weight layout and head, in float32, on the observation
+   * each env waits at and its event's normal draw (as request_obs / request_noise above) — for every
+   * env that ends the launch waiting, at the end of the same launch: policy_action[e] = its squashed
+   * action, policy_ready[e] = SIT_POLICY_READY (never SIT_POLICY_WAITING), *actor_served += the envs
+   * served.  No queue and no capacity: request_env/noise/obs/count/age may be NULL and
+   * request_capacity is ignored.  An env stopped at a sampling event steps again from the start of the
+   * next launch, and every env's rows equal those of the queued path with request_capacity = n_env
+   * and sit_policy_actor, bit for bit.  (Logged launches, which run the one-wave kernel, are served
+   * through the library's own queue of capacity n_env and sit_policy_actor, with the same result.) */
+  const float* actor_weights;  /* float32[SIT_ACTOR_WEIGHTS] (sit_policy_actor's layout) or NULL */
+  int32_t actor_deterministic; /* nonzero: x = mu (no sampling noise) */
+  int64_t* actor_served;       /* int64[1] or NULL: += envs served */
 } sit_rollout_args;
 #define SIT_POLICY_READY 1    /* policy_ready: an action waits in policy_action[e] */
 #define SIT_POLICY_WAITING 2  /* policy_ready: the env stopped at a sampling event for its action */

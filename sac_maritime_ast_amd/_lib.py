@@ -85,6 +85,7 @@ class RolloutArgs(ctypes.Structure):
         ("request_noise", c_void_p), ("request_obs", c_void_p), ("request_count", c_void_p),
         ("request_capacity", c_int32),
         ("env_steps", c_void_p), ("log", c_void_p), ("request_age", c_void_p),
+        ("actor_weights", c_void_p), ("actor_deterministic", c_int32), ("actor_served", c_void_p),
     ]
 
 

@@ -21,26 +21,14 @@
 
 namespace {
 
-constexpr int kActorObs = SIT_OBS_DIM;
-constexpr int kActorHidden = SIT_ACTOR_HIDDEN;
+// (the packed weight layout, f32x2 and the head are sit_serve.h's, shared with the step kernel's
+// in-kernel serving)
 constexpr int kActorRows = 8;
 #ifndef SIT_ACTOR_KB
 #define SIT_ACTOR_KB 8    // W2^T float4 rows per prefetch batch and lane (2 batches in flight): 8 = 144 VGPRs, three
                           // blocks per CU (C5 +2.6 % over 32: 188 VGPRs, two; 16: 168 VGPRs, +1.8 %)
 #endif
 static_assert(64 % SIT_ACTOR_KB == 0 && SIT_ACTOR_KB % 4 == 0, "actor prefetch batch");
-// packed weights (float32): W1 [H][obs] (torch Linear layout), b1 [H], W2^T [H in][H out],
-// b2 [H], W3 [2][H], b3 [2]
-constexpr int kActorW1 = 0;
-constexpr int kActorB1 = kActorW1 + kActorHidden * kActorObs;
-constexpr int kActorW2T = kActorB1 + kActorHidden;
-constexpr int kActorB2 = kActorW2T + kActorHidden * kActorHidden;
-constexpr int kActorW3 = kActorB2 + kActorHidden;
-constexpr int kActorB3 = kActorW3 + 2 * kActorHidden;
-static_assert(kActorB3 + 2 == SIT_ACTOR_WEIGHTS, "packed actor layout");
-static_assert(kActorHidden == 256, "one thread per hidden unit, 256 threads per block");
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_policy_actor(int cap, const float* __restrict__ w, const T* __restrict__ obs,
@@ -165,14 +153,13 @@ __global__ __launch_bounds__(256) void k_policy_actor(int cap, const float* __re
     }
     __syncthreads();
     if (j < nrow) {
-      const float mu = s_part[0][0][2 * j], ls_raw = s_part[0][0][2 * j + 1];
       // normal.py:88-101 (log_sigma clipped to [-20, 2], reparameterised sample), tanh squash
-      const float ls = fminf(fmaxf(ls_raw, -20.0f), 2.0f);
       const int qrow = row0 + j;
-      const float x = deterministic ? mu : fmaf(expf(ls), (float)noise[qrow], mu);
+      const float a = actor_head(s_part[0][0][2 * j], s_part[0][0][2 * j + 1],
+                                 deterministic ? 0.0f : (float)noise[qrow], deterministic != 0);
       const int e = req_env[qrow];
       if (e >= 0 && e < n_env) {
-        policy_action[e] = (T)tanhf(x);
+        policy_action[e] = (T)a;
         policy_ready[e] = 1;
       }
     }

@@ -135,12 +135,15 @@ struct StepIO {
   int32_t transition_capacity;
   int32_t mask_horizon;
   // policy mode (kPolicy): per-env action slots (the request queue is built after the launch by
-  // k_policy_admit, sit_actor.h)
-  const T* policy_action;
+  // k_policy_admit, sit_actor.h, unless the step kernel serves the waiting envs itself: actor_w)
+  T* policy_action;
   int32_t* policy_ready;
   int32_t* request_age;   // [n_env]: admission rounds waited (publish_ages)
   int32_t* group_counts;  // [n_env / 64][kAgeBuckets]: waiting envs per age bucket (handle scratch)
   unsigned long long* env_steps;
+  const float* actor_w;   // in-kernel serving (sit_serve.h): packed actor weights, or null
+  int32_t actor_det;
+  unsigned long long* actor_served;
   T* log;                 // [n_steps][SIT_LOG_ROWS][n_env] or null
 };
 
@@ -550,7 +553,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
     need = a.st.ep_step[env] == 0 || (samp0 >= a.sc.ab_len[env] && a.st.stop[n_env + env] == 0);
     ready = a.io.policy_ready[env] == SIT_POLICY_READY;
     pa = a.io.policy_action[env];
-    if (type == 1) age0 = a.io.request_age[env];
+    if (type == 1) age0 = a.io.request_age ? a.io.request_age[env] : 0;   // (NULL when the launch serves in-kernel)
   }
   if (act) {
     for (int j = 0; j < lo_n; ++j) lo[j] = a.st.last_obs[(size_t)(lo_base + j) * n_env + env];
@@ -1183,7 +1186,7 @@ struct sit_handle {
   // scenario
   unsigned char* scen = nullptr;
   size_t scen_init = 0, scen_end_n = 0, scen_end_e = 0, scen_nw0 = 0, scen_ab_len = 0,
-         scen_ab_alpha = 0, scen_initial = 0, scen_admit = 0, scen_bytes = 0;
+         scen_ab_alpha = 0, scen_initial = 0, scen_admit = 0, scen_serve = 0, scen_bytes = 0;
   // map
   unsigned char* map = nullptr;
   int n_poly = 0, n_vert = 0;
@@ -1432,6 +1435,25 @@ KArgs<T> make_args(const sit_handle* h) {
 
 // policy-mode admission scratch: [n_groups][kAgeBuckets] counts, [n_groups][2] plan, header
 int32_t* admit_counts(const sit_handle* h) { return reinterpret_cast<int32_t*>(h->scen + h->scen_admit); }
+// in-kernel serving's fallback queue (logged launches run the one-wave kernel): capacity n_env
+struct ServeQueue {
+  int32_t* env;
+  int32_t* age;
+  int32_t* count;
+  void* obs;
+  void* noise;
+};
+ServeQueue serve_queue(const sit_handle* h) {
+  unsigned char* b = h->scen + h->scen_serve;
+  const size_t n = (size_t)h->n_env, rs = h->precision == SIT_F64 ? 8 : 4;
+  ServeQueue q;
+  q.env = reinterpret_cast<int32_t*>(b);
+  q.age = q.env + n;
+  q.count = q.age + n;
+  q.obs = b + ((3 * n * 4 + 255) & ~size_t(255));
+  q.noise = static_cast<unsigned char*>(q.obs) + n * SIT_OBS_DIM * rs;
+  return q;
+}
 
 int ready(sit_handle* h) {
   if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
@@ -1464,20 +1486,38 @@ void set_kernel_name(sit_handle* h, bool sync, int mode, bool lds, bool log, int
                 lds ? "map=LDS" : "map=global", log ? "log" : "nolog", mach);
 }
 
+// the launch's k_env_steps_sync map placement and dynamic LDS (0: the launch takes k_env_steps);
+// *attr: the kernel's dynamic-LDS attribute (policy mode: the in-kernel serving size, whether or not
+// the launch serves, so one attribute covers both)
+template <typename T>
+size_t sync_launch_lds(const sit_handle* h, const StepIO<T>& io, bool* lds_map, size_t* attr) {
+  const bool sync_lds = h->lds_map_sel == 1 || (h->lds_map_sel < 0 && io.n_steps >= kLdsMinSteps);
+  const size_t map = sync_lds ? map_stage_bytes(h) : 0;
+  const bool policy = io.policy_action && !io.action_ne;
+  const size_t lds = io.actor_w ? serve_lds_bytes<T>(map) : sync_lds_bytes<T>(map);
+  const size_t at = policy ? serve_lds_bytes<T>(map) : lds;
+  if (lds_map) *lds_map = sync_lds;
+  if (attr) *attr = at;
+  if (h->kernel_classic || io.log || !h->use_index || at + sizeof(Consts<T>) + 256 > kLdsCu) return 0;
+  return lds;
+}
+
 template <typename T>
 int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   KArgs<T> a = make_args<T>(h);
   a.io = io;
   const int mode = io.action_ne ? kExplicit : (io.policy_action ? kPolicy : kSynth);
   const int mach = a.c.mach_simpl ? 1 : 0;
+  if (io.actor_w && mode != kPolicy) return fail(h, SIT_E_INVALID, "in-kernel serving needs policy mode");
   // k_env_steps_sync (sit_sync.h), two waves per ship with the map predicates on their own wave, for
   // every launch without the trajectory log: synthetic sampler (C3/C4), policy (C5) and explicit
   // actions (sit_step, the drop-in MultiShipRLEnv.step).  k_env_steps (one wave per ship) runs the
   // logged launches, and every launch under SIT_STEP_KERNEL=classic.  The sync kernel stages the map
   // into LDS for fused launches; single-step launches read it through the caches.
-  const bool sync_lds = h->lds_map_sel == 1 || (h->lds_map_sel < 0 && io.n_steps >= kLdsMinSteps);
-  const size_t lds_sync = sync_lds ? sync_lds_bytes<T>(map_stage_bytes(h)) : sync_lds_bytes<T>(0);
-  if (!h->kernel_classic && !io.log && h->use_index && lds_sync + sizeof(Consts<T>) + 256 <= kLdsCu) {
+  bool sync_lds = false;
+  size_t lds_attr = 0;
+  const size_t lds_sync = sync_launch_lds<T>(h, io, &sync_lds, &lds_attr);
+  if (lds_sync > 0) {
     const void* kern = nullptr;
     auto pick = [&](auto mode_tag, auto mach_tag, auto lds_tag) {
       constexpr int M = decltype(mode_tag)::value, K = decltype(mach_tag)::value;
@@ -1496,9 +1536,9 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
     else if (mode == kSynth) pick_mach(std::integral_constant<int, kSynth>{});
     else pick_mach(std::integral_constant<int, kExplicit>{});
     const int slot = ((mode * 2 + mach) * 2) + (sync_lds ? 1 : 0);
-    if (h->lds_attr_sync[slot] != (int)lds_sync) {
-      HIP_TRY(h, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sync));
-      h->lds_attr_sync[slot] = (int)lds_sync;
+    if (h->lds_attr_sync[slot] != (int)lds_attr) {
+      HIP_TRY(h, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_attr));
+      h->lds_attr_sync[slot] = (int)lds_attr;
     }
     const int blocks = (h->n_env + kSyncLanes - 1) / kSyncLanes;
     void* args[] = {&a};
@@ -1506,6 +1546,7 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
     set_kernel_name<T>(h, true, mode, sync_lds, false, mach);
     return SIT_OK;
   }
+  if (io.actor_w) return fail(h, SIT_E_INVALID, "in-kernel serving runs on k_env_steps_sync only");
   const int blocks = (h->n_env + kEnvsPerBlock * kGroups - 1) / (kEnvsPerBlock * kGroups);
   // the map (edges, index, classes) is staged in LDS when it fits the budget next to the static
   // exchange buffers and the launch has enough steps to amortise the staging; otherwise the

@@ -266,6 +266,8 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
   // policy-mode admission scratch (sit_actor.h): per 64-env group the age-bucket counts and the plan
   const size_t n_groups = ((size_t)n_env + kAdmitGroup - 1) / kAdmitGroup;
   h->scen_admit = so; so = align256(so + (n_groups * (kAgeBuckets + 2) + 16) * 4);
+  // in-kernel serving's fallback queue (logged policy launches): capacity n_env, zero ages
+  h->scen_serve = so; so = align256(so + (size_t)n_env * (3 * 4 + (SIT_OBS_DIM + 1) * rs) + 256);
   h->scen_bytes = so;
   if (setup_alloc(&h->blob, h->blob_bytes) != hipSuccess || setup_alloc(&h->scen, h->scen_bytes) != hipSuccess) {
     fail(nullptr, SIT_E_NOMEM, "hipMalloc of %zu + %zu bytes failed", h->blob_bytes, h->scen_bytes);
@@ -795,10 +797,15 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     return fail(h, SIT_E_INVALID, "transitions must be aligned to 4 reals");
   if (ra->policy_action && ra->action_ne)
     return fail(h, SIT_E_INVALID, "policy mode and explicit actions are exclusive");
-  if (ra->policy_action && (!ra->policy_ready || !ra->request_env || !ra->request_noise || !ra->request_obs ||
-                            !ra->request_count || !ra->request_age || ra->request_capacity <= 0))
+  const bool serve = ra->policy_action && ra->actor_weights;
+  if (ra->actor_weights && !ra->policy_action) return fail(h, SIT_E_INVALID, "actor_weights need policy mode");
+  if (serve && !ra->policy_ready) return fail(h, SIT_E_INVALID, "policy mode needs policy_ready");
+  if (ra->policy_action && !serve &&
+      (!ra->policy_ready || !ra->request_env || !ra->request_noise || !ra->request_obs || !ra->request_count ||
+       !ra->request_age || ra->request_capacity <= 0))
     return fail(h, SIT_E_INVALID, "policy mode needs policy_ready, request_env, request_noise, "
-                                  "request_obs, request_count, request_age and a positive request_capacity");
+                                  "request_obs, request_count, request_age and a positive request_capacity "
+                                  "(or actor_weights: in-kernel serving)");
   auto fill = [&](auto* io, auto* tag) {
     using R = std::remove_pointer_t<decltype(tag)>;
     io->n_steps = ra->n_steps; io->auto_reset = ra->auto_reset; io->seed = ra->seed;
@@ -808,24 +815,48 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     io->status = ra->status; io->action_out = (R*)ra->action_out; io->done_count = ra->done_count;
     io->transitions = (R*)ra->transitions; io->transition_count = ra->transition_count;
     io->transition_capacity = ra->transition_capacity; io->mask_horizon = ra->mask_horizon;
-    io->policy_action = (const R*)ra->policy_action; io->policy_ready = ra->policy_ready;
-    io->request_age = ra->request_age;
-    io->group_counts = ra->policy_action ? admit_counts(h) : nullptr;
+    // (policy_action: the kernel reads it and, serving, writes it)
+    io->policy_action = const_cast<R*>(static_cast<const R*>(ra->policy_action)); io->policy_ready = ra->policy_ready;
+    io->request_age = serve ? nullptr : ra->request_age;
+    io->group_counts = (ra->policy_action && !serve) ? admit_counts(h) : nullptr;
     io->env_steps = reinterpret_cast<unsigned long long*>(ra->env_steps);
     io->log = (R*)ra->log;
+    io->actor_w = serve ? ra->actor_weights : nullptr;
+    io->actor_det = ra->actor_deterministic;
+    io->actor_served = reinterpret_cast<unsigned long long*>(ra->actor_served);
   };
   // policy mode: the step kernel, then the deterministic admission of the waiting envs into the
-  // request queue (k_policy_admit, sit_actor.h) on the same stream
+  // request queue (k_policy_admit, sit_actor.h) on the same stream — or, serving in the kernel, nothing;
+  // a serving launch that takes the one-wave kernel (logged) is served through the library's own queue
+  auto run = [&](auto* io, auto launch) -> int {
+    using R = std::remove_pointer_t<decltype(io->next_state)>;
+    sit_rollout_args q = *ra;
+    if (serve && sync_launch_lds<R>(h, *io, nullptr, nullptr) == 0) {
+      const ServeQueue sq = serve_queue(h);
+      io->actor_w = nullptr;
+      io->request_age = sq.age;
+      io->group_counts = admit_counts(h);
+      q.request_capacity = h->n_env; q.request_env = sq.env; q.request_obs = sq.obs; q.request_noise = sq.noise;
+      q.request_count = sq.count; q.request_age = sq.age;
+    } else if (serve) {
+      return launch(*io);
+    }
+    int r = launch(*io);
+    if (r == SIT_OK && ra->policy_action) r = launch_policy_admit<R>(h, &q, (hipStream_t)stream);
+    if (r == SIT_OK && serve)
+      r = launch_policy_actor<R>(h, h->n_env, ra->actor_weights, q.request_obs, q.request_noise, q.request_env,
+                                 q.request_count, ra->actor_deterministic, const_cast<void*>(ra->policy_action),
+                                 ra->policy_ready, ra->actor_served, nullptr, (hipStream_t)stream);
+    return r;
+  };
   if (h->precision == SIT_F64) {
     StepIO<double> io{};
     fill(&io, (double*)nullptr);
-    rc = launch_steps<double>(h, io, (hipStream_t)stream);
-    if (rc == SIT_OK && ra->policy_action) rc = launch_policy_admit<double>(h, ra, (hipStream_t)stream);
+    rc = run(&io, [&](const StepIO<double>& x) { return launch_steps<double>(h, x, (hipStream_t)stream); });
   } else {
     StepIO<float> io{};
     fill(&io, (float*)nullptr);
-    rc = launch_steps_f32(h, io, stream);
-    if (rc == SIT_OK && ra->policy_action) rc = launch_policy_admit<float>(h, ra, (hipStream_t)stream);
+    rc = run(&io, [&](const StepIO<float>& x) { return launch_steps_f32(h, x, stream); });
   }
   if (rc) return rc;
   HIP_TRY(h, hipGetLastError());

@@ -23,7 +23,9 @@
 // step in this launch (all four waves skip it: D1 publishes the decision before barrier A), P0 writes
 // the ST_NO_STEP rows, and D1 marks the env SIT_POLICY_WAITING at the end of the launch.  The request
 // queue is built after the launch, deterministically (k_policy_admit, sit_actor.h), from the state
-// the env stopped in.
+// the env stopped in — or, with sit_rollout_args.actor_weights, by the block itself: after barrier C
+// the waiting envs are published to LDS and all four waves evaluate the actor for them
+// (sit_serve.h), so the next launch finds every waiting env's action ready.
 #pragma once
 
 #ifndef SIT_SYNC_LANES
@@ -90,11 +92,14 @@ __host__ __device__ constexpr size_t sync_lds_bytes(size_t map_bytes) {
   return ((map_bytes + 255) & ~size_t(255)) + ((sizeof(SyncShared<T>) + 255) & ~size_t(255));
 }
 
+#include "sit_serve.h"   // in-kernel serving (its LDS layout follows the exchange slots')
+
 // ------------------------------------------------------------------------------------------
 // D waves
 // ------------------------------------------------------------------------------------------
 template <typename T, int MODE, int TYPE, int MACH>
-__device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, SyncShared<T>& X, int env, bool act) {
+__device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, SyncShared<T>& X, ServePub* pub, int env,
+                                      bool act) {
 #if SIT_SYNC_CREF
   const Consts<T>& c = cs;
 #else
@@ -160,7 +165,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       if (MODE == kPolicy) {
         ready = a.io.policy_ready[env] == SIT_POLICY_READY;
         pa = a.io.policy_action[env];
-        age0 = a.io.request_age[env];
+        age0 = a.io.request_age ? a.io.request_age[env] : 0;   // (NULL when the launch serves in-kernel)
       }
     }
   }
@@ -380,11 +385,26 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       a.st.ep_step[env] = ep_step;
       a.st.event[env] = event;
       a.st.episodes[env] = episodes;
-      if (MODE == kPolicy) a.io.policy_ready[env] = ready ? SIT_POLICY_READY : (stalled ? SIT_POLICY_WAITING : 0);
+      // (served in this launch's epilogue: the waiting env's action is ready for the next launch)
+      if (MODE == kPolicy)
+        a.io.policy_ready[env] = (ready || (stalled && pub)) ? SIT_POLICY_READY : (stalled ? SIT_POLICY_WAITING : 0);
     }
   }
   static_assert(kSyncLanes == kAdmitGroup || MODE != kPolicy, "one wave = one admission group");
-  if (MODE == kPolicy && TYPE == 1) publish_ages(a.io.request_age, a.io.group_counts, env, act, stalled, age0);
+  if (MODE == kPolicy && TYPE == 1) {
+    if (pub) {   // in-kernel serving: the waiting envs' ids and their events' normal draws, in lane order
+      const bool w = act && stalled;
+      const unsigned long long m = __ballot(w);
+      if (w) {
+        const int r = (int)__popcll(m & ((1ull << lane) - 1ull));
+        pub->env[r] = env;
+        pub->noise[r] = (float)(T)sampler_normal(a.io.seed, (uint64_t)(a.io.env_id_offset + env), event);
+      }
+      if (lane == 0) pub->count = (int32_t)__popcll(m);
+    } else {
+      publish_ages(a.io.request_age, a.io.group_counts, env, act, stalled, age0);
+    }
+  }
   SY_MARK(13);   // epilogue (the wait at barrier C, the state write-back)
   SY_FLUSH(TYPE);
 }
@@ -394,7 +414,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
 // ------------------------------------------------------------------------------------------
 template <typename T, int MODE, int TYPE, bool LDSMAP>
 __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, const Map<T>& map_in,
-                                      SyncShared<T>& X, int env, bool act) {
+                                      SyncShared<T>& X, ServePub* pub, int env, bool act) {
   const Consts<T> c = cs;   // a register copy (reading the LDS copy where used measured 11 % slower)
   Map<T> map = map_in;
   const int lane = threadIdx.x & (kWave - 1);
@@ -650,6 +670,14 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     if (n >= 1) outputs(n - 1);
     if (act)
       for (int j = 0; j < SIT_OBS_DIM; ++j) a.st.last_obs[(size_t)j * n_env + env] = lo[j];
+    if (MODE == kPolicy && pub) {   // in-kernel serving: the observations the waiting envs wait at
+      const bool w = act && stalled;
+      const unsigned long long m = __ballot(w);
+      if (w) {
+        const int r = (int)__popcll(m & ((1ull << lane) - 1ull));
+        for (int j = 0; j < SIT_OBS_DIM; ++j) pub->obs[r][j] = (float)lo[j];
+      }
+    }
     if (MODE == kPolicy && a.io.env_steps) {   // env-steps executed: one atomic per wave
       unsigned long long v = act ? n_stepped : 0;
       for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
@@ -698,8 +726,17 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
     g[0] = role; g[1] = blockIdx.x; g[2] = 0; g[3] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
   }
 #endif
-  if (role == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, env, act);
-  else if (role == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, env, act);
-  else if (role == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, env, act);
-  else sync_p<T, MODE, 1, LDSMAP>(a, cs, map, X, env, act);
+  // policy mode with in-kernel serving: the published requests after the map and exchange slots
+  // (serve_lds_bytes; the host sized the launch's LDS for it)
+  ServePub* pub = (MODE == kPolicy && a.io.actor_w)
+                      ? reinterpret_cast<ServePub*>(smem + serve_pub_offset<T>(LDSMAP ? (size_t)a.map_bytes : 0))
+                      : nullptr;
+  if (role == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, pub, env, act);
+  else if (role == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, pub, env, act);
+  else if (role == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, pub, env, act);
+  else sync_p<T, MODE, 1, LDSMAP>(a, cs, map, X, pub, env, act);
+  if (MODE == kPolicy && pub) {
+    __syncthreads();   // D: the block's waiting envs published; the map and exchange slots are dead
+    serve_block<T>(a.io.actor_w, a.io.actor_det != 0, smem, *pub, a.io.policy_action, a.io.actor_served);
+  }
 }

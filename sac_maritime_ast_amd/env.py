@@ -181,9 +181,11 @@ class VecMultiShipRLEnv:
         out["transitions"] ([capacity, 24]) and counted in out["transition_count"] ([1]); the count
         is zeroed first unless reset_transitions=False (several launches appending to one buffer).
         policy_io: the policy-mode buffers (see samplers.PolicySampler): actions of sampling events
-        come from a policy run between launches; waiting envs' rows carry status ST_NO_STEP, and
-        after the launch the library admits waiting envs into the request queue, oldest request
-        first, ties by env id (include/sit.h, sit_rollout_args)."""
+        come from a policy; waiting envs' rows carry status ST_NO_STEP.  With "actor_weights" (the
+        packed float32 actor, samplers.pack_actor_weights) the launch serves its waiting envs itself
+        at its end (in-kernel serving; optional "actor_served" int64[1], "actor_deterministic");
+        otherwise after the launch the library admits waiting envs into the request queue
+        ("request_*"), oldest request first, ties by env id (include/sit.h, sit_rollout_args)."""
         n, K = self.n_env, int(n_steps)
         out = {} if out is None else out
         shapes = {"next_state": ((K, n, _lib.SIT_OBS_DIM), self.dtype), "reward": ((K, n), self.dtype),
@@ -230,10 +232,20 @@ class VecMultiShipRLEnv:
         if policy_io is not None:
             if actions is not None:
                 raise ValueError("policy mode and explicit actions are exclusive")
+            serve = policy_io.get("actor_weights") is not None
             for k in ("policy_action", "policy_ready", "request_env", "request_noise", "request_obs",
-                      "request_count", "request_age", "env_steps"):
-                setattr(ra, k, policy_io[k].data_ptr())
-            ra.request_capacity = int(policy_io["request_env"].numel())
+                      "request_count", "request_age", "env_steps", "actor_weights", "actor_served"):
+                t = policy_io.get(k)
+                if t is None and not (serve and k.startswith("request_")) and k not in ("env_steps", "actor_served",
+                                                                                        "actor_weights"):
+                    raise ValueError(f"policy_io needs {k}")
+                setattr(ra, k, None if t is None else t.data_ptr())
+            if serve and (policy_io["actor_weights"].dtype != torch.float32 or
+                          policy_io["actor_weights"].numel() != _lib.SIT_ACTOR_WEIGHTS):
+                raise ValueError("actor_weights: float32[SIT_ACTOR_WEIGHTS] (samplers.pack_actor_weights)")
+            ra.actor_deterministic = int(bool(policy_io.get("actor_deterministic", False)))
+            req = policy_io.get("request_env")
+            ra.request_capacity = 0 if req is None else int(req.numel())
         with torch.cuda.device(self.device):
             _lib.check(self.lib.sit_rollout(self.handle, byref(ra), self._stream()), self.handle)
         return out

@@ -11,15 +11,23 @@ Two action sources, as in ``agent.select_action(state, done, init, mode)`` (main
   evaluated in PyTorch-ROCm between fused K-step launches of the env kernel.
 
 Policy mode on the GPU: an env whose next step is a sampling event and that holds no fresh
-action stops for the rest of the launch.  After the launch the library admits the waiting envs
-into the request queue, oldest request first and ties by env id, at most ``request_capacity`` of
-them (each row: the env's observation and a standard-normal draw keyed by (seed, env id,
-event)); the actor runs on the queued observations and scatters the squashed actions into
-per-env slots; the next launch consumes them.  Each env's trajectory is the one the synchronous
-per-step loop produces (oracle/sit_oracle.py ``OracleEnvs.policy_rollout``;
-tests/test_gpu_policy.py), independent of how envs are batched into launches, and how many rows
-each env executes is a function of the data, the chunk and the capacity (an env waiting since
-launch L is served by round L + ceil(n_env / capacity) - 1), never of GPU scheduling.
+action stops for the rest of the launch.  Its action is computed from its observation and a
+standard-normal draw keyed by (seed, env id, event), in one of two ways:
+
+* in-kernel serving (``serve="kernel"``, the default for the reference's actor architecture): the
+  step kernel itself evaluates the fused actor for every env of a block that ends the launch
+  waiting (csrc/sit_serve.h), so every waiting env steps again from the next launch;
+* the request queue (``serve="queue"``): after the launch the library admits the waiting envs,
+  oldest request first and ties by env id, at most ``request_capacity`` of them; the actor runs
+  on the queued observations (one HIP kernel, or PyTorch-ROCm for other architectures) and
+  scatters the squashed actions into per-env slots (an env waiting since launch L is served by
+  round L + ceil(n_env / capacity) - 1).
+
+The next launch consumes the actions.  Each env's trajectory is the one the synchronous per-step
+loop produces (oracle/sit_oracle.py ``OracleEnvs.policy_rollout``; tests/test_gpu_policy.py),
+independent of how envs are batched into launches, and how many rows each env executes is a
+function of the data, the chunk and the capacity, never of GPU scheduling; both serving paths give
+the same rows bit for bit at capacity n_env.
 ``OverlappedPolicySampler`` splits the envs into groups on separate HIP streams so one group's
 actor runs while the others' env kernels run.
 
@@ -107,51 +115,67 @@ def pack_actor_weights(policy: nn.Module, out: torch.Tensor | None = None) -> to
 
 
 class PolicySampler:
-    """Fused K-step launches in policy mode with the actor evaluated between launches.
+    """Fused K-step launches in policy mode.
 
-    request_capacity bounds the envs served per launch (default n_env: every waiting env);
-    envs beyond it keep waiting, oldest first, for the next admission round.  The actor runs on a
+    serve="kernel" (the default when the actor is fused and no request_capacity is given): the
+    step kernel serves every env that ends a launch waiting, in the same launch (no queue, no
+    capacity).  serve="queue": the actor runs between launches on the request queue;
+    request_capacity bounds the envs served per launch (default n_env: every waiting env) and envs
+    beyond it keep waiting, oldest first, for the next admission round.  The queued actor runs on a
     fixed number of rows (no host synchronisation); rows past the device-side request count are
     scattered into a dummy slot.
 
     With the reference's default actor architecture (``pack_actor_weights``) the whole actor runs as
-    one HIP kernel (sit_policy_actor); ``fused_actor=False`` or any other architecture evaluates the
-    network with PyTorch-ROCm.  The fused path reads a packed copy of the weights: after an
-    optimizer step call ``refresh_weights()`` (``act()`` does it by itself outside HIP-graph
-    replays)."""
+    HIP code (in the step kernel, or sit_policy_actor); ``fused_actor=False`` or any other
+    architecture evaluates the network with PyTorch-ROCm (queue only).  The fused path reads a packed
+    copy of the weights: after an optimizer step call ``refresh_weights()`` (``launch()`` does it by
+    itself outside HIP-graph replays)."""
 
     def __init__(self, env: VecMultiShipRLEnv, policy: nn.Module, chunk: int = 32, seed: int = 25450,
                  env_id_offset: int = 0, request_capacity: int | None = None, mask_horizon: int = 600,
                  transition_capacity: int = 0, deterministic: bool = False, actor_dtype=None,
-                 fused_actor: bool = True):
+                 fused_actor: bool = True, serve: str | None = None):
         self.env, self.policy, self.chunk, self.seed = env, policy, int(chunk), int(seed)
         self.env_id_offset, self.mask_horizon = int(env_id_offset), int(mask_horizon)
         self.transition_capacity, self.deterministic = int(transition_capacity), deterministic
         n, dev, dt = env.n_env, env.device, env.dtype
-        cap = int(request_capacity or n)
-        if cap <= 0:
-            raise ValueError("request_capacity must be positive")
         self.actor_dtype = actor_dtype or next(policy.parameters()).dtype
+        self._w = pack_actor_weights(policy) if fused_actor and self.actor_dtype == torch.float32 else None
+        if serve is None:
+            serve = "kernel" if self._w is not None and request_capacity is None else "queue"
+        if serve not in ("kernel", "queue"):
+            raise ValueError("serve must be 'kernel' or 'queue'")
+        if serve == "kernel" and (self._w is None or request_capacity is not None):
+            raise ValueError("in-kernel serving needs the fused actor (the reference's architecture, float32) "
+                             "and serves every waiting env (no request_capacity)")
+        self.serve = serve
+        self.served = torch.zeros(1, dtype=torch.int64, device=dev)   # policy evaluations used
         self.io = {
             "policy_action": torch.zeros(n + 1, dtype=dt, device=dev),      # slot n: dummy
             "policy_ready": torch.zeros(n + 1, dtype=torch.int32, device=dev),
-            "request_env": torch.zeros(cap, dtype=torch.int32, device=dev),
-            "request_noise": torch.zeros(cap, dtype=dt, device=dev),
-            "request_obs": torch.zeros((cap, _lib.SIT_OBS_DIM), dtype=dt, device=dev),
-            # rows admitted by the last launch (written by the library's admission kernel)
-            "request_count": torch.zeros(1, dtype=torch.int32, device=dev),
-            # admission rounds each waiting env has waited (kept by the admission kernel)
-            "request_age": torch.zeros(n, dtype=torch.int32, device=dev),
             "env_steps": torch.zeros(1, dtype=torch.int64, device=dev),
         }
-        self._rows = torch.arange(cap, device=dev, dtype=torch.int32)
-        self._one = torch.full((cap,), _lib.SIT_POLICY_READY, dtype=torch.int32, device=dev)
-        self.out: dict = {}
-        self.served = torch.zeros(1, dtype=torch.int64, device=dev)   # policy evaluations used
-        self._w = pack_actor_weights(policy) if fused_actor and self.actor_dtype == torch.float32 else None
         if self._w is not None:
             self._w = self._w.to(dev)
             self._w_version = self._weights_version()
+        if serve == "kernel":
+            self.io.update(actor_weights=self._w, actor_served=self.served, actor_deterministic=bool(deterministic))
+        else:
+            cap = int(request_capacity or n)
+            if cap <= 0:
+                raise ValueError("request_capacity must be positive")
+            self.io.update({
+                "request_env": torch.zeros(cap, dtype=torch.int32, device=dev),
+                "request_noise": torch.zeros(cap, dtype=dt, device=dev),
+                "request_obs": torch.zeros((cap, _lib.SIT_OBS_DIM), dtype=dt, device=dev),
+                # rows admitted by the last launch (written by the library's admission kernel)
+                "request_count": torch.zeros(1, dtype=torch.int32, device=dev),
+                # admission rounds each waiting env has waited (kept by the admission kernel)
+                "request_age": torch.zeros(n, dtype=torch.int32, device=dev),
+            })
+            self._rows = torch.arange(cap, device=dev, dtype=torch.int32)
+            self._one = torch.full((cap,), _lib.SIT_POLICY_READY, dtype=torch.int32, device=dev)
+        self.out: dict = {}
 
     @property
     def fused(self) -> bool:
@@ -173,11 +197,15 @@ class PolicySampler:
 
     def launch(self, want=("next_state", "reward", "done", "status", "action"), events=None,
                first: bool = True):
-        """One fused launch of `chunk` steps followed by the actor on the queued requests.
+        """One fused launch of `chunk` steps, serving its waiting envs in the kernel, or followed by
+        the actor on the queued requests.
         Returns the launch's [K, n_env, ...] outputs (rows of waiting envs: status ST_NO_STEP).
         events: optional (start, end) torch.cuda.Event pair recorded around the env kernel.
         first: the launch starts a new batch of replay transitions (their count is zeroed); later
         launches of a batch append to it, so a HIP graph of several launches keeps all of them."""
+        if (self.serve == "kernel" and not torch.cuda.is_current_stream_capturing()
+                and self._weights_version() != self._w_version):
+            self.refresh_weights()
         if events is not None:
             events[0].record(torch.cuda.current_stream(self.env.device))
         self.env.rollout(self.chunk, seed=self.seed, env_id_offset=self.env_id_offset, out=self.out,
@@ -185,11 +213,12 @@ class PolicySampler:
                          mask_horizon=self.mask_horizon, policy_io=self.io, reset_transitions=first)
         if events is not None:
             events[1].record(torch.cuda.current_stream(self.env.device))
-        self.act()
+        if self.serve == "queue":
+            self.act()
         return self.out
 
     def capture(self, n_launch: int = 2, want=("next_state", "reward", "done", "status", "action")):
-        """Record `n_launch` launches (env kernel + admission + actor) into one HIP graph; replay()
+        """Record `n_launch` launches (env kernel [+ admission + actor]) into one HIP graph; replay()
         then runs them with a single submission (the per-launch host work of ctypes and ~10 torch
         ops otherwise bounds short chunks).  The output buffers are those of the last launch."""
         if n_launch < 1:
@@ -213,8 +242,10 @@ class PolicySampler:
         one HIP kernel (sit_policy_actor) for the default architecture; otherwise the network in
         PyTorch-ROCm, then the squashed Gaussian head and the scatter in one HIP kernel
         (sit_policy_apply), or for policies without a `.net` (mu, log_sigma) trunk forward() and a
-        device-side scatter."""
+        device-side scatter.  (Queue serving only: in-kernel serving has nothing left to do.)"""
         io, env = self.io, self.env
+        if self.serve == "kernel":
+            return
         if self._w is not None:
             if not torch.cuda.is_current_stream_capturing() and self._weights_version() != self._w_version:
                 self.refresh_weights()

@@ -604,3 +604,124 @@ def test_f64_intermediate_waypoint_sampler_switches_to_policy():
     assert n >= 200, n
     ref = o.policy_rollout(n, SEED, oracle_policy_fn(make_policy(torch.float64, "cpu")))
     compare(seq, ref, n_env, n)
+
+
+# ------------------------------------------------------------------------------------------
+# in-kernel serving (sit_rollout_args.actor_weights): the step kernel evaluates the actor for the
+# envs of each block that end the launch waiting (csrc/sit_serve.h)
+# ------------------------------------------------------------------------------------------
+def _same(a, b):
+    """Bitwise equal, NaN where NaN (the route-angle column of non-event rows)."""
+    return torch.equal(torch.isnan(a), torch.isnan(b)) and torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
+
+
+def _serving_samplers(n, precision, chunk, serves, deterministic=False, seed=77, tcap=0):
+    pol = make_policy256(DEV)
+    out = []
+    for serve in serves:
+        env = VecMultiShipRLEnv(scenario=make_scenario(n, cap=48, seed=seed), precision=precision, device=DEV)
+        env.reset()
+        env.init_step()
+        out.append(PolicySampler(env, pol, chunk=chunk, seed=SEED, serve=serve, deterministic=deterministic,
+                                 transition_capacity=tcap))
+    return pol, out
+
+
+@pytest.mark.parametrize("precision", [32, 64])
+def test_in_kernel_serving_equals_queue_path(precision):
+    """In-kernel serving against the request queue at capacity n_env served by sit_policy_actor, from
+    the same start: every launch's rows (next_state, reward, done, status, action), the action slots
+    and ready flags, the replay transitions, and the served / env-step counters are identical bit for
+    bit (include/sit.h: both paths share the actor's per-row arithmetic), and no env ever waits more
+    than the launch it stopped in."""
+    n, chunk, n_launch = (2048, 32, 12) if precision == 32 else (512, 32, 10)
+    _, (k, q) = _serving_samplers(n, precision, chunk, ("kernel", "queue"), tcap=chunk * n // 32)
+    assert k.serve == "kernel" and q.serve == "queue"
+    assert "request_env" not in k.io
+    prev_wait = np.zeros(n, dtype=bool)
+    for it in range(n_launch):
+        ok, oq = k.launch(), q.launch()
+        torch.cuda.synchronize()
+        for key in ("done", "status"):
+            assert torch.equal(ok[key], oq[key]), f"launch {it}: {key}"
+        live = (ok["status"].to(torch.int64) & _lib.ST_NO_STEP) == 0   # (ST_NO_STEP rows are not written)
+        for key in ("next_state", "reward", "action"):
+            assert _same(ok[key][live], oq[key][live]), f"launch {it}: {key}"
+        assert torch.equal(k.io["policy_action"][:n], q.io["policy_action"][:n]), f"launch {it}: actions"
+        rk, rq = k.io["policy_ready"][:n].cpu().numpy(), q.io["policy_ready"][:n].cpu().numpy()
+        assert np.array_equal(rk, rq), f"launch {it}: ready flags"
+        assert not (rk == _lib.SIT_POLICY_WAITING).any()
+        ck, cq = int(ok["transition_count"].item()), int(oq["transition_count"].item())
+        assert ck == cq, f"launch {it}: transitions {ck} vs {cq}"
+        tk = ok["transitions"][:ck].cpu().numpy()
+        tq = oq["transitions"][:cq].cpu().numpy()
+        tk, tq = tk[np.lexsort(tk.T[::-1])], tq[np.lexsort(tq.T[::-1])]
+        assert np.array_equal(tk, tq), f"launch {it}: transition records"
+        st = ok["status"].to(torch.int64).cpu().numpy() & 0xFFFFFFFF
+        waiting = ((st & _lib.ST_NO_STEP) != 0).all(0)
+        assert not (waiting & prev_wait).any(), f"launch {it}: an env waited two launches in a row"
+        prev_wait = waiting
+    assert int(k.served.item()) == int(q.served.item()) >= n
+    assert int(k.env_steps.item()) == int(q.env_steps.item())
+
+
+@pytest.mark.parametrize("precision,deterministic", [(32, False), (32, True), (64, False)])
+def test_in_kernel_serving_actions_match_torch_float64(precision, deterministic):
+    """The actions the step kernel serves against the same policy in float64 PyTorch on each served
+    env's observation (state last_obs) and its event's normal draw (oracle sampler_normal): |error|
+    <= 1e-5; the served counter advances by the envs served (all envs waiting at the end of the
+    launch; the ready flags are cleared before each launch so that every env at an event waits)."""
+    n = 2048
+    pol, (k,) = _serving_samplers(n, precision, 32, ("kernel",), deterministic=deterministic, seed=7)
+    ref_pol = copy.deepcopy(pol).double()
+    checked = 0
+    for it in range(6):
+        k.io["policy_ready"].zero_()
+        before = int(k.served.item())
+        k.launch()
+        torch.cuda.synchronize()
+        served = np.nonzero(k.io["policy_ready"][:n].cpu().numpy() == _lib.SIT_POLICY_READY)[0]
+        assert int(k.served.item()) - before == served.size
+        st = _np_state(k.env)
+        obs = torch.from_numpy(st["last_obs"].T[served].astype(np.float64)).to(DEV)
+        ev = st["event"][served].astype(np.uint32)
+        noise = torch.from_numpy(np.asarray(so.sampler_normal(SEED, served.astype(np.uint64), ev))).to(DEV)
+        with torch.no_grad():
+            ref = ref_pol(obs, noise, deterministic=deterministic)[0][:, 0]
+        got = k.io["policy_action"][torch.from_numpy(served).to(DEV)].double()
+        if served.size:
+            err = (got - ref).abs().max().item()
+            assert err <= 1e-5, f"launch {it}: served action max |err| {err:.3e} over {served.size} envs"
+            assert ref.abs().max().item() > (1e-3 if deterministic else 0.05)
+        checked += served.size
+    assert checked >= n
+
+
+def test_in_kernel_serving_logged_launch_takes_library_queue():
+    """A logged policy launch runs the one-wave kernel, which cannot serve in-kernel: the library
+    serves it through its own queue (capacity n_env) and sit_policy_actor.  Float64: the logged run's
+    done / status rows and ready flags equal the unlogged (in-kernel) run's, launch by launch, its
+    reals within 1e-9 (the two step kernels' float64 contract) and its served actions within 1e-6
+    (float32 actor on observations equal to 1e-9)."""
+    n, chunk = 256, 16
+    _, (a, b) = _serving_samplers(n, 64, chunk, ("kernel", "kernel"), seed=21)
+    for it in range(8):
+        oa = a.env.rollout(chunk, seed=SEED, out=a.out, policy_io=a.io, log=True,
+                           want=("next_state", "reward", "done", "status", "action"))
+        name = a.env.lib.sit_step_kernel(a.env.handle).decode()
+        ob = b.launch()
+        torch.cuda.synchronize()
+        assert name.startswith("k_env_steps<") and "log" in name, name
+        for key in ("done", "status"):
+            assert torch.equal(oa[key], ob[key]), f"launch {it}: {key}"
+        live = (oa["status"].to(torch.int64) & _lib.ST_NO_STEP) == 0
+        for key, floor in (("next_state", torch.tensor(OBS_SCALE, device=DEV)), ("reward", 1.0),
+                           ("action", torch.tensor([1e4, 1e4, np.pi, 1.0], device=DEV, dtype=torch.float64))):
+            x, y = oa[key][live], ob[key][live]
+            assert torch.equal(torch.isnan(x), torch.isnan(y)), f"launch {it}: {key} NaN pattern"
+            err = (torch.nan_to_num(x) - torch.nan_to_num(y)).abs() / torch.maximum(
+                torch.nan_to_num(y).abs(), torch.as_tensor(floor, device=DEV, dtype=y.dtype).expand_as(y))
+            assert err.numel() == 0 or err.max().item() <= 1e-9, f"launch {it}: {key} rel err {err.max().item():.3e}"
+        assert (a.io["policy_action"][:n] - b.io["policy_action"][:n]).abs().max().item() <= 1e-6, f"launch {it}"
+        assert torch.equal(a.io["policy_ready"][:n], b.io["policy_ready"][:n]), f"launch {it}: ready"
+    assert int(a.served.item()) == int(b.served.item()) > 0
