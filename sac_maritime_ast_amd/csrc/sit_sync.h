@@ -708,6 +708,9 @@ template <typename T, int MODE, int MACH, bool LDSMAP>
 __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ Consts<T> cs;
+#ifdef SIT_DIAG_SYNC
+  const unsigned long long sy_k0 = __builtin_amdgcn_s_memtime();
+#endif
   for (int i = threadIdx.x; i < (int)(sizeof(Consts<T>) / 4); i += blockDim.x)
     reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
   const Map<T> map = LDSMAP ? stage_map(a, smem) : a.map;
@@ -718,6 +721,9 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
   const bool act = lane < kSyncLanes && env < a.n_env;
   SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(smem + (LDSMAP ? (((size_t)a.map_bytes + 255) & ~size_t(255)) : 0));
   __syncthreads();   // constants copied, map staged
+#ifdef SIT_DIAG_SYNC   // slot 15: kernel start to the staged map (per launch)
+  if (lane == 0) atomicAdd(&g_sit_diag[role >> 1][(role & 1) * 16 + 15], __builtin_amdgcn_s_memtime() - sy_k0);
+#endif
 #ifdef SIT_DIAG_PLACE
   if (lane == 0 && blockIdx.x * 4 + w < kDiagWaves) {   // which SIMD each role's wave sits on
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);     // HW_REG_HW_ID
@@ -736,7 +742,13 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
   else if (role == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, pub, env, act);
   else sync_p<T, MODE, 1, LDSMAP>(a, cs, map, X, pub, env, act);
   if (MODE == kPolicy && pub) {
+#ifdef SIT_DIAG_SYNC
+    const unsigned long long sy_s0 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();   // D: the block's waiting envs published; the map and exchange slots are dead
     serve_block<T>(a.io.actor_w, a.io.actor_det != 0, smem, *pub, a.io.policy_action, a.io.actor_served);
+#ifdef SIT_DIAG_SYNC   // slot 14: the wait at barrier D and the serving (per launch)
+    if (lane == 0) atomicAdd(&g_sit_diag[role >> 1][(role & 1) * 16 + 14], __builtin_amdgcn_s_memtime() - sy_s0);
+#endif
   }
 }

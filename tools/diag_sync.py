@@ -6,7 +6,8 @@ never shipped):
     SIT_LIBRARY=build_diag/libsit_diagsync.so python tools/diag_sync.py [--policy]
 
 Runs the bench workload (f32, 32768 envs, synthetic sampler, auto-reset; --policy: one group in policy
-mode with the fused actor) and prints, per role (D0 test-ship dynamics, D1 obstacle dynamics, P0 / P1
+mode with the fused actor served in the step kernel, 64 steps per launch; --queue: on the request queue)
+and prints, per role (D0 test-ship dynamics, D1 obstacle dynamics, P0 / P1
 their position predicates and outputs), shader cycles per wave-step: work before barrier A, the wait
 at A, work A -> B, the wait at B, work after B.  The s_memtime stamps cost ~10 % themselves."""
 import argparse
@@ -32,7 +33,8 @@ SUB = {"D": {10: ("work before A", "Euler position"), 8: ("work A->B", "dynamics
        "P": {6: ("work A->B", "P0 outputs up to the row stores"), 7: ("work A->B", "P0 outputs after the stores"),
              8: ("work A->B", "cell record + first edges"), 9: ("work A->B", "boundary distance"),
              10: ("work A->B", "hull test")}}
-ONCE = {12: "prologue (per launch)", 13: "epilogue (per launch)"}
+ONCE = {12: "prologue (per launch)", 13: "epilogue (per launch)", 14: "barrier D + in-kernel serving (per launch)",
+        15: "kernel start to the staged map (per launch)"}
 ROLES = ["D0 test dynamics", "D1 obstacle dynamics", "P0 test predicates+outputs", "P1 obstacle predicates"]
 
 
@@ -42,6 +44,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=2000)
     ap.add_argument("--launches", type=int, default=5)
     ap.add_argument("--policy", action="store_true")
+    ap.add_argument("--queue", action="store_true", help="--policy on the request queue (capacity n/4)")
+    ap.add_argument("--policy-chunk", type=int, default=64)
     ap.add_argument("--step", action="store_true", help="explicit actions, one launch per step (sit_step)")
     args = ap.parse_args()
     lib = ctypes.CDLL(_lib.LIB_PATH)
@@ -64,7 +68,8 @@ def main():
     elif args.policy:
         from sac_maritime_ast_amd.samplers import GaussianPolicy, PolicySampler
         torch.manual_seed(0)
-        sm = PolicySampler(env, GaussianPolicy().to("cuda:0"), chunk=64, request_capacity=args.n_env // 4)
+        sm = PolicySampler(env, GaussianPolicy().to("cuda:0"), chunk=args.policy_chunk,
+                           request_capacity=args.n_env // 4 if args.queue else None)
         run = sm.launch
         for _ in range(600):
             run()
