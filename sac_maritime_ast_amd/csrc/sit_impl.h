@@ -1494,7 +1494,9 @@ size_t sync_launch_lds(const sit_handle* h, const StepIO<T>& io, bool* lds_map, 
   const bool sync_lds = h->lds_map_sel == 1 || (h->lds_map_sel < 0 && io.n_steps >= kLdsMinSteps);
   const size_t map = sync_lds ? map_stage_bytes(h) : 0;
   const bool policy = io.policy_action && !io.action_ne;
-  const size_t lds = io.actor_w ? serve_lds_bytes<T>(map) : sync_lds_bytes<T>(map);
+  const size_t lds = io.actor_w ? serve_lds_bytes<T>(map)
+                     : policy   ? sync_lds_bytes<T, kPolicy>(map)
+                     : io.action_ne ? sync_lds_bytes<T, kExplicit>(map) : sync_lds_bytes<T, kSynth>(map);
   const size_t at = policy ? serve_lds_bytes<T>(map) : lds;
   if (lds_map) *lds_map = sync_lds;
   if (attr) *attr = at;

@@ -111,12 +111,12 @@ static_assert(sizeof(f32x2) * (kServeRows / 2) * kActorHidden == sizeof(float) *
               "layer-2 activations alias h1");
 
 __host__ __device__ constexpr size_t serve_align(size_t b) { return (b + 255) & ~size_t(255); }
-// the dynamic LDS of a serving launch: [map | exchange slots] (or the actor's working set, whichever
-// is larger), then the published requests
+// the dynamic LDS of a serving launch: [map | exchange slots | transition ring] (or the actor's
+// working set, whichever is larger), then the published requests
 template <typename T>
 __host__ __device__ constexpr size_t serve_pub_offset(size_t map_bytes) {
-  return sync_lds_bytes<T>(map_bytes) > serve_align(sizeof(ServeWork)) ? sync_lds_bytes<T>(map_bytes)
-                                                                       : serve_align(sizeof(ServeWork));
+  return sync_lds_bytes<T, kPolicy>(map_bytes) > serve_align(sizeof(ServeWork)) ? sync_lds_bytes<T, kPolicy>(map_bytes)
+                                                                                : serve_align(sizeof(ServeWork));
 }
 template <typename T>
 __host__ __device__ constexpr size_t serve_lds_bytes(size_t map_bytes) {

@@ -87,9 +87,23 @@ struct SyncShared {
   SyncSlot<T> d[2];
 };
 
-template <typename T>
+// P0's replay-transition ring (records of sampling events, SIT_TRANSITION_DIM reals each): buffered
+// in LDS and appended to the caller's buffer by one atomic per flush.  (One atomic per step with
+// events made P0 wait for the slot on its critical segment — and, gfx9 counting stores in vmcnt,
+// for the reward / done / status stores issued just before it: C3 paid 4.8 % for the stream; the ring
+// measured C3 +2.3 %.)  Synthetic-sampler launches only: policy launches are 64 steps long, and the
+// ring's last flush put an atomic round trip before their serving barrier (C5 -2.7 %); they append
+// per step (kTrRing 0).
+template <int MODE>
+constexpr int kTrRing = MODE == kSynth ? 64 : 0;
+template <typename T, int MODE>
+__host__ __device__ constexpr size_t sync_ring_bytes() {
+  return ((size_t)kTrRing<MODE> * SIT_TRANSITION_DIM * sizeof(T) + 255) & ~size_t(255);
+}
+// the sync kernel's dynamic LDS: [staged map | exchange slots | transition ring]
+template <typename T, int MODE>
 __host__ __device__ constexpr size_t sync_lds_bytes(size_t map_bytes) {
-  return ((map_bytes + 255) & ~size_t(255)) + ((sizeof(SyncShared<T>) + 255) & ~size_t(255));
+  return ((map_bytes + 255) & ~size_t(255)) + ((sizeof(SyncShared<T>) + 255) & ~size_t(255)) + sync_ring_bytes<T, MODE>();
 }
 
 #include "sit_serve.h"   // in-kernel serving (its LDS layout follows the exchange slots')
@@ -414,7 +428,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
 // ------------------------------------------------------------------------------------------
 template <typename T, int MODE, int TYPE, bool LDSMAP>
 __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, const Map<T>& map_in,
-                                      SyncShared<T>& X, ServePub* pub, int env, bool act) {
+                                      SyncShared<T>& X, ServePub* pub, T* ring, int env, bool act) {
   const Consts<T> c = cs;   // a register copy (reading the LDS copy where used measured 11 % slower)
   Map<T> map = map_in;
   const int lane = threadIdx.x & (kWave - 1);
@@ -475,6 +489,23 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   int* p_dc = (TYPE == 0 && (uf & kUfDoneCnt)) ? a.io.done_count : nullptr;
 
   SY_MARK(12);   // prologue
+  // P0: the transition ring's records appended to the caller's buffer (one atomic for all of them;
+  // records past transition_capacity are counted, not written)
+  constexpr int kRing = kTrRing<MODE>;
+  int ring_n = 0;                   // records in the ring (wave-uniform)
+  auto flush = [&]() {
+    if (ring_n == 0) return;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(a.io.transition_count, ring_n);
+    base = __shfl(base, 0);
+    const int tcap = a.io.transition_capacity;
+    for (int i = lane; i < ring_n * (SIT_TRANSITION_DIM / 4); i += kWave) {
+      const int r = i / (SIT_TRANSITION_DIM / 4), q = i - r * (SIT_TRANSITION_DIM / 4);
+      const T* src = ring + (size_t)r * SIT_TRANSITION_DIM + 4 * q;
+      if (base + r < tcap) store4(a.io.transitions + (size_t)(base + r) * SIT_TRANSITION_DIM + 4 * q, src[0], src[1], src[2], src[3]);
+    }
+    ring_n = 0;
+  };
   // P0: reward, done, status, replay transition and done count of step j (MSRL_env_ex.py:906-980);
   // called once per step, in order
   auto outputs = [&](int j) {
@@ -491,10 +522,14 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
         ++n_stepped;
       }
     }
+    // (outside the live branch: the transition ring is driven with every lane active — its flush
+    // copies by all 64 lanes and lane 0 takes the slots)
+    T nt[6], no[4];
+    T reward = T(0);
+    bool sac = false;
     if (live) {
       // every LDS value of the step read up front (one wait; the empty asm keeps the reads out of
       // the branches below)
-      T nt[6], no[4];
       for (int q = 0; q < 6; ++q) nt[q] = xd.t[q][lane];
       for (int q = 0; q < 4; ++q) no[q] = xd.o[q][lane];
       const uint32_t bo = xd.bo[lane], f1 = xd.f[1][lane];
@@ -506,42 +541,49 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       const T snt = (T(1) - xsqrt(dn * dn + de * de) * c.inv_maxn) * T(0.001);
       const T r_snt = (bo & kStopBit) ? T(0) : snt;
       const T rs = coll ? T(2000) : T(0);
-      const T reward = r_nt_t + r_term_t + r_nto + r_o + r_snt + rs;
+      reward = r_nt_t + r_term_t + r_nto + r_o + r_snt + rs;
       const uint32_t status = ((bits_t | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
       if (uf & 2) *p_rw = reward;
       if (uf & 4) *p_dn = env_done ? 1 : 0;
       if (uf & 8) *p_st = status;
-      SY_MARK(6);
-      const bool sac = (f1 & kSfSac) != 0;
-      if (uf & kUfTrans) {             // replay transition of a sampling event (main_ast.py:385-396)
-        const unsigned long long m = __ballot(sac);
-        if (m) {
-          const int lead = __builtin_ctzll(m);
+      sac = (f1 & kSfSac) != 0;
+    }
+    SY_MARK(6);
+    if (uf & kUfTrans) {               // replay transition of a sampling event (main_ast.py:385-396)
+      const unsigned long long m = __ballot(sac);
+      if (m) {
+        const int nn = (int)__popcll(m), rank = (int)__popcll(m & ((1ull << lane) - 1ull));
+        if (kRing > 0 && ring_n + nn > kRing) flush();
+        T* rec = nullptr;
+        if (kRing > 0 && nn <= kRing) {  // into the ring
+          if (sac) rec = ring + (size_t)(ring_n + rank) * SIT_TRANSITION_DIM;
+          ring_n += nn;
+        } else {                         // a burst larger than the ring: appended directly
           int base = 0;
-          if (lane == lead) base = atomicAdd(a.io.transition_count, (int)__popcll(m));
-          base = __shfl(base, lead);
-          const int slot = base + (int)__popcll(m & ((1ull << lane) - 1ull));
-          if (sac && slot < a.io.transition_capacity) {
-            // the 24-real record (include/sit.h) as six 4-real stores (a record starts 4-real aligned)
-            T* rec = a.io.transitions + (size_t)slot * SIT_TRANSITION_DIM;
-            const bool horizon_hit = (uf & kUfMaskH) && xd.ep[lane] + 2 == a.io.mask_horizon;
-            const T mask = (horizon_hit || !env_done) ? T(1) : T(0);
-            store4(rec, lo[0], lo[1], lo[2], lo[3]);
-            store4(rec + 4, lo[4], lo[5], lo[6], lo[7]);
-            store4(rec + 8, lo[8], lo[9], xd.o[4][lane], reward);
-            store4(rec + 12, nt[0], nt[1], nt[2], nt[3]);
-            store4(rec + 16, nt[4], nt[5], no[0], no[1]);
-            store4(rec + 20, no[2], no[3], mask, (T)(a.io.env_id_offset + env));
-          }
+          if (lane == 0) base = atomicAdd(a.io.transition_count, nn);
+          base = __shfl(base, 0);
+          if (sac && base + rank < a.io.transition_capacity)
+            rec = a.io.transitions + (size_t)(base + rank) * SIT_TRANSITION_DIM;
+        }
+        if (rec) {
+          // the 24-real record (include/sit.h) as six 4-real stores (a record starts 4-real aligned)
+          const bool horizon_hit = (uf & kUfMaskH) && xd.ep[lane] + 2 == a.io.mask_horizon;
+          const T mask = (horizon_hit || !env_done) ? T(1) : T(0);
+          store4(rec, lo[0], lo[1], lo[2], lo[3]);
+          store4(rec + 4, lo[4], lo[5], lo[6], lo[7]);
+          store4(rec + 8, lo[8], lo[9], xd.o[4][lane], reward);
+          store4(rec + 12, nt[0], nt[1], nt[2], nt[3]);
+          store4(rec + 16, nt[4], nt[5], no[0], no[1]);
+          store4(rec + 20, no[2], no[3], mask, (T)(a.io.env_id_offset + env));
         }
       }
-      // (the observation before the next step: every step when transitions or policy requests read
-      // it, else only at the last step, for last_obs)
-      if (MODE == kPolicy || (uf & kUfTrans) || j == n - 1) {
-        const bool restart = (uf & kUfAutoReset) && env_done;   // the auto reset's initial observation
-        for (int q = 0; q < 6; ++q) lo[q] = restart ? li[q] : nt[q];
-        for (int q = 0; q < 4; ++q) lo[6 + q] = restart ? li[6 + q] : no[q];
-      }
+    }
+    // (the observation before the next step: every step when transitions or policy requests read
+    // it, else only at the last step, for last_obs)
+    if (live && (MODE == kPolicy || (uf & kUfTrans) || j == n - 1)) {
+      const bool restart = (uf & kUfAutoReset) && env_done;   // the auto reset's initial observation
+      for (int q = 0; q < 6; ++q) lo[q] = restart ? li[q] : nt[q];
+      for (int q = 0; q < 4; ++q) lo[6 + q] = restart ? li[6 + q] : no[q];
     }
     if (uf & kUfDoneCnt) {
       const unsigned long long m = __ballot(env_done);
@@ -668,6 +710,7 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   __syncthreads();   // C
   if (TYPE == 0) {
     if (n >= 1) outputs(n - 1);
+    if (kRing > 0 && (uf & kUfTrans)) flush();
     if (act)
       for (int j = 0; j < SIT_OBS_DIM; ++j) a.st.last_obs[(size_t)j * n_env + env] = lo[j];
     if (MODE == kPolicy && pub) {   // in-kernel serving: the observations the waiting envs wait at
@@ -737,10 +780,12 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
   ServePub* pub = (MODE == kPolicy && a.io.actor_w)
                       ? reinterpret_cast<ServePub*>(smem + serve_pub_offset<T>(LDSMAP ? (size_t)a.map_bytes : 0))
                       : nullptr;
+  // P0's transition ring after the exchange slots
+  T* ring = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(&X) + ((sizeof(SyncShared<T>) + 255) & ~size_t(255)));
   if (role == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, pub, env, act);
   else if (role == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, pub, env, act);
-  else if (role == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, pub, env, act);
-  else sync_p<T, MODE, 1, LDSMAP>(a, cs, map, X, pub, env, act);
+  else if (role == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, pub, ring, env, act);
+  else sync_p<T, MODE, 1, LDSMAP>(a, cs, map, X, pub, ring, env, act);
   if (MODE == kPolicy && pub) {
 #ifdef SIT_DIAG_SYNC
     const unsigned long long sy_s0 = __builtin_amdgcn_s_memtime();
