@@ -725,3 +725,62 @@ def test_in_kernel_serving_logged_launch_takes_library_queue():
         assert (a.io["policy_action"][:n] - b.io["policy_action"][:n]).abs().max().item() <= 1e-6, f"launch {it}"
         assert torch.equal(a.io["policy_ready"][:n], b.io["policy_ready"][:n]), f"launch {it}: ready"
     assert int(a.served.item()) == int(b.served.item()) > 0
+
+
+def test_f32_c5_size_in_kernel_serving_graph_replay():
+    """Config C5 as bench.py runs it by default: 65 536 ships (2 groups x 16 384 envs, two streams), the
+    256x256 actor served inside the step kernel, 16 launches per HIP graph.  Properties: executed rows
+    account for the device env-step counter, ST_NO_STEP rows carry done 0, outputs are finite, every env
+    is served; no env takes no step in two launches in a row; and batching independence: the first 512
+    envs of a 16 384-env handle and of a 512-env handle (same global ids and policy) execute identical
+    rows, launch by launch."""
+    n, G, chunk, per_graph = 16384, 2, 64, 16
+    pol = make_policy256(DEV)
+    samplers = []
+    for g in range(G):
+        env = VecMultiShipRLEnv(scenario=make_scenario(n, cap=48, seed=25450, env_offset=g * n), precision=32,
+                                device=DEV)
+        env.reset()
+        env.init_step()
+        samplers.append(PolicySampler(env, pol, chunk=chunk, seed=SEED, env_id_offset=g * n,
+                                      transition_capacity=per_graph * chunk * n // 64))
+    assert all(s.serve == "kernel" for s in samplers)
+    ov = OverlappedPolicySampler(samplers).capture(per_graph)
+    before = [int(s.env_steps.item()) for s in samplers]
+    for rep in range(3):
+        outs = ov.replay()
+        torch.cuda.synchronize()
+        for s, out in zip(samplers, outs):
+            st = out["status"].to(torch.int64) & 0xFFFFFFFF
+            live = (st & _lib.ST_NO_STEP) == 0
+            assert torch.isfinite(out["next_state"][live]).all() and torch.isfinite(out["reward"][live]).all()
+            assert not out["done"][~live].any()
+            assert not (s.io["policy_ready"][:n] == _lib.SIT_POLICY_WAITING).any()
+    stepped = [int(s.env_steps.item()) - b for s, b in zip(samplers, before)]
+    for s in stepped:
+        assert s > 0.8 * 3 * per_graph * chunk * n, stepped
+    for s in samplers:
+        assert int(s.served.item()) > n
+    m, n_launch = 512, 10
+    rows = []
+    for nn in (n, m):
+        env = VecMultiShipRLEnv(scenario=make_scenario(nn, cap=48, seed=25450, env_offset=0), precision=32,
+                                device=DEV)
+        env.reset()
+        env.init_step()
+        sm = PolicySampler(env, pol, chunk=chunk, seed=SEED, env_id_offset=0)
+        outs, prev = [], np.zeros(m, dtype=bool)
+        for _ in range(n_launch):
+            o = sm.launch()
+            torch.cuda.synchronize()
+            outs.append({k: o[k][:, :m].cpu().numpy().copy() for k in ("next_state", "reward", "status", "done")})
+            st = outs[-1]["status"].astype(np.int64) & 0xFFFFFFFF
+            waited = ((st & _lib.ST_NO_STEP) != 0).all(0)
+            assert not (waited & prev).any(), "an env took no step in two launches in a row"
+            prev = waited
+        rows.append(outs)
+    for i, (x, y) in enumerate(zip(*rows)):
+        assert np.array_equal(x["status"], y["status"]) and np.array_equal(x["done"], y["done"]), f"launch {i}"
+        live = ((x["status"].astype(np.int64) & _lib.ST_NO_STEP) == 0)
+        assert np.array_equal(x["next_state"][live], y["next_state"][live]), f"launch {i}: next_state"
+        assert np.array_equal(x["reward"][live], y["reward"][live]), f"launch {i}: reward"
