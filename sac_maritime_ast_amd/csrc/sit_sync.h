@@ -735,6 +735,25 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   SY_FLUSH(2 + TYPE);
 }
 
+// Issue priority per role (s_setprio 0-3).  The two blocks on a CU put their waves on the SIMDs in
+// D/P pairs of different env groups, and the two waves of a SIMD compete for its issue slots where
+// both are ready.  The P waves carry the step's longest chains (P0: the previous step's outputs and
+// the test ship's map predicates before barrier B), the D waves have slack (D0 most): a total order
+// by that load — P0 > P1 > D1 > D0 — measured C3 +3.3 % and C5 +4.8 % (same-box A/B, two rounds;
+// favouring the D waves instead cost 1 - 2 %, giving both P waves the same level lost the gain on C3)
+#ifndef SIT_PRIO_P0
+#define SIT_PRIO_P0 3
+#endif
+#ifndef SIT_PRIO_P1
+#define SIT_PRIO_P1 2
+#endif
+#ifndef SIT_PRIO_D1
+#define SIT_PRIO_D1 1
+#endif
+#ifndef SIT_PRIO_D0
+#define SIT_PRIO_D0 0
+#endif
+
 // LDSMAP: the island map staged into LDS per block (fused launches) or read through the caches
 // (single-step launches, whose prologue cannot amortise staging 57 KB per block)
 // SIT_SYNC_WAVES_PER_EU: the occupancy the kernel's registers are allocated for (waves per SIMD; 0 = the
@@ -782,6 +801,12 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
                       : nullptr;
   // P0's transition ring after the exchange slots
   T* ring = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(&X) + ((sizeof(SyncShared<T>) + 255) & ~size_t(255)));
+  {  // the role's issue priority (s_setprio, SIT_PRIO_*)
+    constexpr int prio[4] = {SIT_PRIO_D0, SIT_PRIO_D1, SIT_PRIO_P0, SIT_PRIO_P1};
+    if (prio[role] == 1) __builtin_amdgcn_s_setprio(1);
+    else if (prio[role] == 2) __builtin_amdgcn_s_setprio(2);
+    else if (prio[role] == 3) __builtin_amdgcn_s_setprio(3);
+  }
   if (role == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, pub, env, act);
   else if (role == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, pub, env, act);
   else if (role == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, pub, ring, env, act);
