@@ -36,6 +36,26 @@
 #endif
 constexpr int kSyncLanes = SIT_SYNC_LANES;
 
+// Issue priority per role (s_setprio 0-3).  The two blocks on a CU put their waves on the SIMDs in
+// D/P pairs of different env groups, and the two waves of a SIMD compete for its issue slots where
+// both are ready.  The P waves carry the step's longest chains (P0: the previous step's outputs and
+// the test ship's map predicates before barrier B), the D waves have slack (D0 most): a total order
+// by that load — P0 > P1 > D1 > D0 — measured C3 +3.3 % and C5 +4.8 % (same-box A/B, two rounds;
+// favouring the D waves instead cost 1 - 2 %, giving both P waves the same level lost the gain on C3)
+#ifndef SIT_PRIO_P0
+#define SIT_PRIO_P0 3
+#endif
+#ifndef SIT_PRIO_P1
+#define SIT_PRIO_P1 2
+#endif
+#ifndef SIT_PRIO_D1
+#define SIT_PRIO_D1 1
+#endif
+#ifndef SIT_PRIO_D0
+#define SIT_PRIO_D0 0
+#endif
+
+
 // SIT_DIAG_SYNC (diagnostic builds only, tools/diag_sync.py): shader cycles per role and loop segment,
 // lane 0 of each wave, summed into g_sit_diag[role >> 1][(role & 1) * 16 + segment]: 0 work before
 // barrier A, 1 wait at A, 2 work A -> B, 3 wait at B, 4 work after B, 5 wave-steps; 6 and 7 P0's
@@ -361,6 +381,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     SY_MARK(2);
     __syncthreads();   // B: both ships' step and their map predicates
     SY_MARK(3);
+#ifdef SIT_PRIO_D1_B   // (experiment) D1's priority from barrier B to barrier A
+    if (TYPE == 1) __builtin_amdgcn_s_setprio(SIT_PRIO_D1_B);
+#endif
     // the episode's end (every predicate, the collision) and the auto reset (main_ast.py:314-333)
     if (act && !stalled) {
       const uint32_t pb0 = xd.pb[0][lane], pb1 = xd.pb[1][lane];
@@ -387,6 +410,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     }
     SY_MARK(4);
     SY_STEP();
+#ifdef SIT_PRIO_D1_B
+    if (TYPE == 1) __builtin_amdgcn_s_setprio(SIT_PRIO_D1);
+#endif
   }
   __syncthreads();   // C: P1's reward terms of the last step (P0 writes that step's outputs)
   if (act) {
@@ -641,6 +667,9 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     SY_MARK(2);
     __syncthreads();   // B: the D waves' step results
     SY_MARK(3);
+#ifdef SIT_PRIO_P1_B   // (experiment) P1's priority from barrier B to barrier A
+    if (TYPE == 1) __builtin_amdgcn_s_setprio(SIT_PRIO_P1_B);
+#endif
     if (act && !stalled) {
       const uint32_t fl = xd.f[TYPE][lane];
       int stop = (fl & kSfStopPre) ? 1 : 0;
@@ -704,6 +733,9 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     }
     p_ns += row_step * SIT_OBS_DIM;
     p_ao += row_step * 4;
+#ifdef SIT_PRIO_P1_B
+    if (TYPE == 1) __builtin_amdgcn_s_setprio(SIT_PRIO_P1);
+#endif
     SY_MARK(4);
     SY_STEP();
   }
@@ -734,25 +766,6 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   SY_MARK(13);   // epilogue (the wait at barrier C, P0's last outputs and last_obs)
   SY_FLUSH(2 + TYPE);
 }
-
-// Issue priority per role (s_setprio 0-3).  The two blocks on a CU put their waves on the SIMDs in
-// D/P pairs of different env groups, and the two waves of a SIMD compete for its issue slots where
-// both are ready.  The P waves carry the step's longest chains (P0: the previous step's outputs and
-// the test ship's map predicates before barrier B), the D waves have slack (D0 most): a total order
-// by that load — P0 > P1 > D1 > D0 — measured C3 +3.3 % and C5 +4.8 % (same-box A/B, two rounds;
-// favouring the D waves instead cost 1 - 2 %, giving both P waves the same level lost the gain on C3)
-#ifndef SIT_PRIO_P0
-#define SIT_PRIO_P0 3
-#endif
-#ifndef SIT_PRIO_P1
-#define SIT_PRIO_P1 2
-#endif
-#ifndef SIT_PRIO_D1
-#define SIT_PRIO_D1 1
-#endif
-#ifndef SIT_PRIO_D0
-#define SIT_PRIO_D0 0
-#endif
 
 // LDSMAP: the island map staged into LDS per block (fused launches) or read through the caches
 // (single-step launches, whose prologue cannot amortise staging 57 KB per block)
