@@ -784,3 +784,47 @@ def test_f32_c5_size_in_kernel_serving_graph_replay():
         live = ((x["status"].astype(np.int64) & _lib.ST_NO_STEP) == 0)
         assert np.array_equal(x["next_state"][live], y["next_state"][live]), f"launch {i}: next_state"
         assert np.array_equal(x["reward"][live], y["reward"][live]), f"launch {i}: reward"
+
+
+def test_rollout_serving_argument_checks():
+    """sit_rollout's policy-mode argument rules (include/sit.h), checked before anything is launched:
+    actor_weights need policy mode and policy_ready; without actor_weights every request buffer and a
+    positive capacity are required; policy mode and explicit actions are exclusive.  A serving launch
+    with the request buffers left NULL is accepted."""
+    import ctypes
+    n = 128
+    env = VecMultiShipRLEnv(scenario=make_scenario(n, cap=32, seed=3), precision=32, device=DEV)
+    env.reset()
+    env.init_step()
+    w = torch.zeros(_lib.SIT_ACTOR_WEIGHTS, dtype=torch.float32, device=DEV)
+    act = torch.zeros(n + 1, dtype=torch.float32, device=DEV)
+    ready = torch.zeros(n + 1, dtype=torch.int32, device=DEV)
+    ns = torch.empty((1, n, _lib.SIT_OBS_DIM), dtype=torch.float32, device=DEV)
+    ane = torch.zeros((1, n, 2), dtype=torch.float32, device=DEV)
+    u8 = torch.zeros((1, n), dtype=torch.uint8, device=DEV)
+
+    def call(**kw):
+        ra = _lib.RolloutArgs()
+        ra.n_steps, ra.auto_reset, ra.seed = 1, 1, 1
+        ra.next_state = ns.data_ptr()
+        for k, v in kw.items():
+            setattr(ra, k, v)
+        with torch.cuda.device(DEV):
+            rc = env.lib.sit_rollout(env.handle, ctypes.byref(ra), env._stream())
+        return rc, env.lib.sit_last_error(env.handle)
+
+    rc, msg = call(actor_weights=w.data_ptr())
+    assert rc == _lib.SIT_E_INVALID and b"policy mode" in msg
+    rc, msg = call(actor_weights=w.data_ptr(), policy_action=act.data_ptr())
+    assert rc == _lib.SIT_E_INVALID and b"policy_ready" in msg
+    rc, msg = call(policy_action=act.data_ptr(), policy_ready=ready.data_ptr())
+    assert rc == _lib.SIT_E_INVALID and b"request_capacity" in msg
+    rc, msg = call(policy_action=act.data_ptr(), policy_ready=ready.data_ptr(), actor_weights=w.data_ptr(),
+                   action_ne=ane.data_ptr(), sac_update=u8.data_ptr(), init=u8.data_ptr())
+    assert rc == _lib.SIT_E_INVALID and b"exclusive" in msg
+    rc, msg = call(policy_action=act.data_ptr(), policy_ready=ready.data_ptr(), actor_weights=w.data_ptr())
+    torch.cuda.synchronize()
+    assert rc == 0, msg
+    assert "kPolicy" in env.lib.sit_step_kernel(env.handle).decode()
+    # every env started at its episode's first sampling event with no action: served in the same launch
+    assert (ready[:n] == _lib.SIT_POLICY_READY).all()
