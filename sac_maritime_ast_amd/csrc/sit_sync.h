@@ -779,6 +779,14 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
 #else
 #define SIT_SYNC_OCC
 #endif
+// SIT_SIMD_ROLES (experiment): roles by the SIMD a wave runs on (HW_ID), mirrored for the second
+// block of a CU (a per-CU ticket), so that every SIMD holds one D and one P wave
+#ifndef SIT_SIMD_ROLES
+#define SIT_SIMD_ROLES 0
+#endif
+#if SIT_SIMD_ROLES
+__device__ int g_cu_ticket[2048];
+#endif
 template <typename T, int MODE, int MACH, bool LDSMAP>
 __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -790,12 +798,26 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
     reinterpret_cast<uint32_t*>(&cs)[i] = reinterpret_cast<const uint32_t*>(&a.c)[i];
   const Map<T> map = LDSMAP ? stage_map(a, smem) : a.map;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int role = (blockIdx.x & 1) == 0 ? w : (w ^ 2);
+#if SIT_SIMD_ROLES
+  __shared__ int s_tk;
+  if (threadIdx.x == 0) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);     // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);   // HW_REG_XCC_ID
+    const unsigned key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) & 2047;
+    s_tk = atomicAdd(&g_cu_ticket[key], 1) & 1;
+  }
+#endif
   const int lane = threadIdx.x & (kWave - 1);
   const int env = blockIdx.x * kSyncLanes + lane;
   const bool act = lane < kSyncLanes && env < a.n_env;
   SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(smem + (LDSMAP ? (((size_t)a.map_bytes + 255) & ~size_t(255)) : 0));
   __syncthreads();   // constants copied, map staged
+#if SIT_SIMD_ROLES
+  const int simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) >> 4) & 3);
+  const int role = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readfirstlane(s_tk) ? (simd ^ 2) : simd);
+#else
+  const int role = (blockIdx.x & 1) == 0 ? w : (w ^ 2);
+#endif
 #ifdef SIT_DIAG_SYNC   // slot 15: kernel start to the staged map (per launch)
   if (lane == 0) atomicAdd(&g_sit_diag[role >> 1][(role & 1) * 16 + 15], __builtin_amdgcn_s_memtime() - sy_k0);
 #endif
