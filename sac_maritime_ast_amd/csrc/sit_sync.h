@@ -779,10 +779,15 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
 #else
 #define SIT_SYNC_OCC
 #endif
-// SIT_SIMD_ROLES (experiment): roles by the SIMD a wave runs on (HW_ID), mirrored for the second
-// block of a CU (a per-CU ticket), so that every SIMD holds one D and one P wave
+// Roles by SIMD (fused launches): a block's four waves sit on four different SIMDs and a CU holds two
+// blocks (i and i + 256), so fixed roles by wave index left a quarter of the SIMDs with two D waves and
+// a quarter with two P waves.  Each wave takes its role from the SIMD it runs on (HW_ID), mirrored for
+// the second block of its CU (a per-CU ticket, one atomic per block while the map stages), so every SIMD
+// holds one D and one P wave — which the issue priorities above then order.  Measured C3 +3.3 % with the
+// priorities (without them, round 3: -0.3 %), C5 unchanged.  Single-step launches (map through the
+// caches, nothing staged to hide the ticket's round trip behind) keep the fixed order.
 #ifndef SIT_SIMD_ROLES
-#define SIT_SIMD_ROLES 0
+#define SIT_SIMD_ROLES 1
 #endif
 #if SIT_SIMD_ROLES
 __device__ int g_cu_ticket[2048];
@@ -800,7 +805,7 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #if SIT_SIMD_ROLES
   __shared__ int s_tk;
-  if (threadIdx.x == 0) {
+  if (LDSMAP && threadIdx.x == 0) {
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);     // HW_REG_HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);   // HW_REG_XCC_ID
     const unsigned key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) & 2047;
@@ -814,7 +819,8 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
   __syncthreads();   // constants copied, map staged
 #if SIT_SIMD_ROLES
   const int simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) >> 4) & 3);
-  const int role = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readfirstlane(s_tk) ? (simd ^ 2) : simd);
+  const int role = LDSMAP ? __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readfirstlane(s_tk) ? (simd ^ 2) : simd)
+                          : ((blockIdx.x & 1) == 0 ? w : (w ^ 2));
 #else
   const int role = (blockIdx.x & 1) == 0 ? w : (w ^ 2);
 #endif
