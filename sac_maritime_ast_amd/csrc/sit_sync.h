@@ -819,7 +819,10 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
   __syncthreads();   // constants copied, map staged
 #if SIT_SIMD_ROLES
   const int simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) >> 4) & 3);
-  const int role = LDSMAP ? __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readfirstlane(s_tk) ? (simd ^ 2) : simd)
+#ifndef SIT_SIMD_MIRROR
+#define SIT_SIMD_MIRROR 2   // the second block's roles: simd ^ 2 pairs (D0, P0), (D1, P1); ^ 3 pairs (D0, P1), (D1, P0)
+#endif
+  const int role = LDSMAP ? __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readfirstlane(s_tk) ? (simd ^ SIT_SIMD_MIRROR) : simd)
                           : ((blockIdx.x & 1) == 0 ? w : (w ^ 2));
 #else
   const int role = (blockIdx.x & 1) == 0 ? w : (w ^ 2);
