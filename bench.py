@@ -85,6 +85,14 @@ def parse():
     ap.add_argument("--c5-warmup", type=int, default=32 * 16 * 60, help="warm-up steps of the C5 line")
     ap.add_argument("--c5-groups", type=int, default=1, help="C5 line: stream groups (1 measured fastest)")
     ap.add_argument("--c5-chunk", type=int, default=64, help="C5 line: env steps per launch")
+    ap.add_argument("--no-extra-lines", action="store_true",
+                    help="rollout mode: skip the secondary lines (C3 in float64, C5 with the PyTorch-ROCm actor)")
+    ap.add_argument("--trajectory-stride", type=int, default=0,
+                    help="rollout mode: also gather every S-th step's trajectory rows (next_state, reward, done, "
+                         "status) of every rank to rank 0 per launch (shard.TrajectoryGather; 0 = off)")
+    ap.add_argument("--torch-actor", action="store_true",
+                    help="policy mode: the actor forward in PyTorch-ROCm on the request queue (north_star's C5 "
+                         "wording) instead of the fused HIP actor")
     args = ap.parse_args()
     if args.chunk is None:
         args.chunk = 32 if args.mode == "policy" else 40000
@@ -346,7 +354,7 @@ def launch_plan(args, chunk):
 def bench_rollout(args, rank, world, dev):
     """Configs C3/C4: synthetic random-IW sampler on device, fused `chunk`-step launches."""
     from sac_maritime_ast_amd import VecMultiShipRLEnv, make_scenario
-    from sac_maritime_ast_amd.shard import AsyncTransitionGather, shard_offset
+    from sac_maritime_ast_amd.shard import AsyncTransitionGather, TrajectoryGather, shard_offset
 
     n_env = args.n_env
     offset = shard_offset(rank, n_env)
@@ -371,6 +379,9 @@ def bench_rollout(args, rank, world, dev):
     # gathers them (at N = 1 rank 0 is the learner: the count crosses to the host, no record moves)
     gather = AsyncTransitionGather(tcap, 24, env.dtype, dev, world) if (args.mode == "rollout" and not args.no_gather) \
         else None
+    # optional: strided trajectory rows of every rank to the learner, behind each launch
+    tgather = (TrajectoryGather(chunk, n_env, args.trajectory_stride, env.dtype, dev, world)
+               if args.mode == "rollout" and getattr(args, "trajectory_stride", 0) > 0 else None)
     out = {}
     launch_no = [0]
 
@@ -406,13 +417,18 @@ def bench_rollout(args, rank, world, dev):
             if gather:     # counts now, the valid records once this launch's counts are on the host
                 gather.start(i)
                 gather.progress(i - 1)
+            if tgather:
+                tgather.start(out)
             launch_no[0] += 1
 
     for _ in range(warm // chunk):
         one()
     if gather:
         gather.finish()
+    if tgather:
+        tgather.wait()
     gathered0, dropped0 = (gather.gathered, gather.dropped()) if gather else (0, 0)
+    tbytes0 = tgather.bytes_moved if tgather else 0
     n_launch = steps // chunk
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
 
@@ -421,6 +437,8 @@ def bench_rollout(args, rank, world, dev):
             one(ev[i])
         if gather:
             gather.finish()
+        if tgather:
+            tgather.wait()
     elapsed = timed(dev, world, run)
     launch_ms = [a.elapsed_time(b) for a, b in ev]
     if args.launch_trace:
@@ -453,6 +471,10 @@ def bench_rollout(args, rank, world, dev):
         "roofline": rl,
         "roofline_valu": roofline_valu(kern_ms, pmc, n_env, chunk) if args.mode == "rollout" else None,
     }
+    if tgather is not None:
+        res["config"]["rccl_trajectory_gather"] = {
+            "to": "rank 0", "stride": args.trajectory_stride, "rows_per_launch_per_rank": tgather.rows,
+            "fields": list(TrajectoryGather.FIELDS), "bytes_received_timed": tgather.bytes_moved - tbytes0}
     if gather is not None:
         stats = torch.tensor([gather.gathered - gathered0, gather.dropped() - dropped0], dtype=torch.float64,
                              device=dev)
@@ -493,7 +515,8 @@ def bench_policy(args, rank, world, dev):
         env.init_step()
         cap = None if args.serve == "kernel" else max(256, per // args.request_div)
         samplers.append(PolicySampler(env, policy, chunk=chunk, seed=args.seed, env_id_offset=off,
-                                      request_capacity=cap, transition_capacity=tcap, serve=args.serve))
+                                      request_capacity=cap, transition_capacity=tcap, serve=args.serve,
+                                      fused_actor=not getattr(args, "torch_actor", False)))
     runner = OverlappedPolicySampler(samplers) if G > 1 else None
     cur = torch.cuda.current_stream(dev)
     # kernel duration of the env launches: eager launches through the sampler (HIP events on each
@@ -598,6 +621,26 @@ def main():
         a5.mode, a5.chunk, a5.groups = "policy", args.c5_chunk, args.c5_groups
         a5.steps, a5.warmup = max(args.c5_steps, a5.chunk * 16 * 2), args.c5_warmup
         c5 = bench_policy(a5, rank, world, dev)
+    extra = {}
+    if args.mode == "rollout" and not args.no_extra_lines and args.precision == 32:
+        # secondary lines (not the headline): C3 in the reference's own float64 arithmetic, and C5 with the
+        # actor forward in PyTorch-ROCm on the request queue, two stream groups (north_star's C5 wording)
+        a64 = argparse.Namespace(**vars(args))
+        a64.precision, a64.chunk, a64.steps, a64.warmup = 64, 10000, 30000, 40000
+        r64 = bench_rollout(a64, rank, world, dev)
+        extra["c3_f64"] = {"metric": "env-steps/sec, 65 536 ships per GPU, float64 (the reference's arithmetic)",
+                           "value": r64["value"], "unit": "env-steps/s", "dtype": "f64", "steps": r64["steps"],
+                           "warmup": r64["warmup"], "ms_per_step": r64["ms_per_step"], "config": r64["config"],
+                           "roofline": r64["roofline"]}
+        if not args.no_c5:
+            at = argparse.Namespace(**vars(args))
+            at.mode, at.chunk, at.groups, at.serve, at.torch_actor = "policy", 32, 2, "queue", True
+            at.steps, at.warmup = 32 * 16 * 8, 32 * 16 * 30
+            rt = bench_policy(at, rank, world, dev)
+            extra["c5_torch_actor"] = {
+                "metric": "env-steps/sec, 65 536 policy-driven ships per GPU (config C5), PyTorch-ROCm actor",
+                "value": rt["value"], "unit": "env-steps/s", "steps": rt["steps"], "warmup": rt["warmup"],
+                "ms_per_step": rt["ms_per_step"], "config": rt["config"], "roofline": rt["roofline"]}
     result = {"metric": METRIC, "value": r["value"], "unit": "env-steps/s", "n_gpus": world, "steps": r["steps"],
               "warmup": r["warmup"], "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
               "vs_baseline": None, "dtype": "f32" if args.precision == 32 else "f64",
@@ -609,6 +652,7 @@ def main():
         result["c5"] = {"metric": "env-steps/sec, 65 536 policy-driven ships per GPU (config C5)", "value": c5["value"],
                         "unit": "env-steps/s", "steps": c5["steps"], "warmup": c5["warmup"],
                         "ms_per_step": c5["ms_per_step"], "config": c5["config"], "roofline": c5["roofline"]}
+    result.update(extra)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.seed, args.cpu_baseline_workers)
     if rank == 0:

@@ -265,20 +265,30 @@ int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint
 /* Self-test of the IEEE float64 helpers the knife-edge decisions use (diagnostic; no reference
  * counterpart): out[i] = op(a[i], b[i]) with op 0 a / b, 1 sqrt(a), 2 a*a + b*b, 3 (a + b) - a,
  * 4 a*b + b*a (each correctly rounded per operation, as numpy's float64), 5 sin(a), 6 cos(a),
- * 7 atan2(a, b) (the device math library the float64 path uses).  fast_tu != 0 runs the copy
- * compiled with the float32 step kernels' fast-math flags.  Device pointers. */
+ * 7 atan2(a, b) (the device math library the float64 path uses), 8 the fused step kernel's wave
+ * roles (sync_role_of) for the SIMD assignment a (base 4, digit v = SIMD of wave v) and CU ticket b,
+ * packed as role of wave v in base-4 digit v.  fast_tu != 0 runs the copy compiled with the float32
+ * step kernels' fast-math flags.  Device pointers. */
 int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, double* out, int32_t fast_tu,
                      void* stream);
 /* Debug builds (libsit_debug.so, compiled with -DSIT_DEBUG; no reference counterpart): every table
  * index the step kernels compute is bounds-checked; a failed check sets bit i of the returned word
  * (0 route-table row, 1 next-waypoint index, 2 route length, 3 spatial-index entry or range, 4 edge
- * id, 5 class-grid word, 6 mixed-cell record or live-edge range), and every table read it guards is
+ * id, 5 class-grid word, 6 mixed-cell record or live-edge range, 7 in-kernel serving: a block's
+ * published request count outside [0, 64] or its LDS past the launch's dynamic LDS, 8 in-kernel
+ * serving: a served env id outside [0, n_env)), and every table read or write it guards is
  * clamped into its table (indices to a valid entry, ranges to their in-table part; the next-waypoint
  * and route-length checks guard the route-table rows of bit 0), so the launch completes without an
  * out-of-bounds access.  sit_debug_flags synchronises the device, returns the bits set since the last
  * call and clears them; release builds return 0.  sit_debug_build: 1 in a debug build. */
 int sit_debug_flags(uint32_t* flags);
 int32_t sit_debug_build(void);
+/* Placement record of the fused two-wave step kernel (no reference counterpart): the number of
+ * blocks, since the last reset, whose four waves did not sit on four different SIMDs.  Roles are a
+ * permutation of D0, D1, P0, P1 for every placement (results never depend on it); the count shows
+ * how often the issue-priority pairing the kernel is tuned for was not available.  Synchronises the
+ * device; reset != 0 clears the count. */
+int sit_role_fallbacks(uint64_t* count, int32_t reset);
 /* Put every env into its construction-time state (as if freshly built).  Unlike
  * sit_reset this also re-initialises the shaft speed and all controller integrators. */
 int sit_restart(sit_handle* h, void* stream);

@@ -107,6 +107,7 @@ SIGNATURES = {
     "sit_step_kernel": (c_char_p, [c_void_p]),
     "sit_debug_flags": (c_int32, [c_void_p]),
     "sit_debug_build": (c_int32, []),
+    "sit_role_fallbacks": (c_int32, [c_void_p, c_int32]),
     "sit_load_map": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "sit_load_routes": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "sit_load_initial": (c_int32, [c_void_p, c_void_p]),

@@ -492,9 +492,11 @@ class MultiShipRLEnv:
         self._blob_t = torch.zeros(self.vec._state_bytes, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
         self._host_state = {k: v.numpy() for k, v in self.vec._views(self._blob_t).items()}
         ptr = lambda a: c_void_p(a.ctypes.data)  # noqa: E731
+        # (the array pointers are cached; the stream is the caller's current one, taken per call under
+        # the handle's device, so a step is ordered after a reset or state write on the same stream)
         self._step_args = (self.vec.handle, ptr(self._act), ptr(self._sac), ptr(self._init), ptr(self._ns),
                            ptr(self._rw), ptr(self._dn), ptr(self._st), ptr(self._log) if self.record else None,
-                           c_void_p(self._blob_t.data_ptr()) if self.record else None, self.vec._stream())
+                           c_void_p(self._blob_t.data_ptr()) if self.record else None)
         self._step_fn = self.vec.lib.sit_step_host
         r = scenario.routes[0, 1]
         nw = int(scenario.n_wpt[0, 1])
@@ -574,7 +576,8 @@ class MultiShipRLEnv:
         a[1] = converted_action[1]
         self._sac[0] = 1 if SAC_update else 0
         self._init[0] = 1 if init else 0
-        rc = self._step_fn(*self._step_args)
+        with torch.cuda.device(self.vec.device):
+            rc = self._step_fn(*self._step_args, self.vec._stream())
         if rc:
             _lib.check(rc, self.vec.handle)
         # recording envs have the post-step state on the host; otherwise a view fetches it on demand

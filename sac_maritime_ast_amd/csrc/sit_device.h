@@ -102,6 +102,9 @@ enum DebugCheck {
   kDbgEdgeId = 4,        // an edge id >= the map's edge count
   kDbgClassWord = 5,     // a class-grid word outside the grid
   kDbgCellRecord = 6,    // a mixed-cell record or live-edge entry outside its table
+  kDbgServeCount = 7,    // in-kernel serving: a published request count outside [0, 64], or the serving
+                         // LDS (ServeWork, ServePub) past the launch's dynamic LDS
+  kDbgServeEnv = 8,      // in-kernel serving: a published env id outside [0, n_env)
 };
 #ifdef SIT_DEBUG
 namespace {
@@ -134,6 +137,30 @@ __device__ __forceinline__ int dbg_span(int first, int cnt, int n, int id) {
 #define SIT_DEDGE(m, i) SIT_DCLAMP((int)(i), (m).n_edge, kDbgEdgeId)
 
 constexpr int kWave = 64;         // CDNA wavefront
+
+// The role (0 D0, 1 D1, 2 P0, 3 P1) of wave w of a k_env_steps_sync block from the SIMDs its four waves
+// sit on (simd[v] = HW_ID SIMD of wave v) and the block's CU ticket (tk: the second block of a CU
+// mirrors): the rank of (simd[w], w) among the block's four (simd, wave) pairs, XOR mirror for tk = 1.
+// Always a permutation of the four roles, whatever the placement (the pairs are distinct and totally
+// ordered); equal to simd[w] (^ mirror) when the four SIMDs differ, the placement the issue
+// priorities are tuned for.  (Dispatch gives no guarantee of that placement: MI355X_MICROARCH.md.)
+#ifndef SIT_SIMD_ROLES
+#define SIT_SIMD_ROLES 1    // fused k_env_steps_sync launches take their roles by SIMD (sit_sync.h)
+#endif
+#ifndef SIT_SIMD_MIRROR
+#define SIT_SIMD_MIRROR 2   // the second block's roles: ^ 2 pairs (D0, P0), (D1, P1); ^ 3 pairs (D0, P1), (D1, P0)
+#endif
+__host__ __device__ constexpr int sync_role_of(int s0, int s1, int s2, int s3, int w, int tk, int mirror) {
+  const int s[4] = {s0, s1, s2, s3};
+  const int me = s[w];
+  int rank = 0;
+  for (int v = 0; v < 4; ++v) rank += (s[v] < me || (s[v] == me && v < w)) ? 1 : 0;
+  return tk ? (rank ^ mirror) : rank;
+}
+// whether the four SIMDs are pairwise different (the placement the roles are tuned for)
+__host__ __device__ constexpr bool sync_simds_distinct(int s0, int s1, int s2, int s3) {
+  return ((1 << (s0 & 3)) | (1 << (s1 & 3)) | (1 << (s2 & 3)) | (1 << (s3 & 3))) == 0xF;
+}
 #ifndef SIT_ENVS_PER_BLOCK
 #define SIT_ENVS_PER_BLOCK 64
 #endif
@@ -455,10 +482,67 @@ struct Ship {
   T hi, hp;                  // heading PID integral and previous error
   T ect_int;                 // LOS cross-track integral
   T lrpm, lect, lpme;        // last stored observations (stop path)
+  // float32: the low parts of the integrators (comp_add): the value is n + ln etc.  float64: unused
+  T ln, le, lpsi, li1, li2, lhi, lei;
   int k;                     // next waypoint index
   int ticks;                 // simulator time in dt units
   int stop;                  // ShipAssets.stop_flag
 };
+
+// Integrators of the float32 handle as double-float values (hi + lo).  The reference integrates in
+// float64; a float32 sum x += dx loses up to half an ulp of x every step, and for the integrators that
+// nothing pulls back — the position along the track (ulp 4.9e-4 m at 4-8 km), the shaft-speed PI
+// integral (1e5-1e6, ulp 0.008-0.06), the heading and the other PI/PID and LOS integrals, the sampling
+// distance — those losses random-walk: 1e-3 - 1e-2 m of position after 2 000 steps, which moved
+// waypoint switches, sampling events and terrain contacts (profiles/r04_f32_flip_attribution.json).
+// comp_add carries each step's rounding error in lo and adds it back with the next increment
+// (compensated summation, Fast2Sum: |hi| >= |inc| for all but zero crossings, where the terms are
+// small): hi stays the float32-rounded running sum and the error no longer accumulates.  The
+// decisions read hi + lo in float64 (comp_val).  float64 handles: the plain sum.
+template <typename T>
+__device__ __forceinline__ T comp_add(T hi, T& lo, T inc) {
+  if constexpr (kIsF32<T>) {
+#pragma clang fp reassociate(off) contract(off)
+    const T y = inc + lo;
+    const T t = hi + y;
+    lo = y - (t - hi);
+    return t;
+  } else {
+    (void)lo;
+    return hi + inc;
+  }
+}
+// hi + a * b as comp_add, the product fused into the low part's update (one rounding, one extra
+// dependent instruction on the integrator's chain: t = hi + fma(a, b, lo))
+template <typename T>
+__device__ __forceinline__ T comp_fma(T hi, T& lo, T a, T b) {
+  if constexpr (kIsF32<T>) {
+#pragma clang fp reassociate(off) contract(off)
+    const T y = __builtin_fmaf(a, b, lo);
+    const T t = hi + y;
+    lo = y - (t - hi);
+    return t;
+  } else {
+    (void)lo;
+    return hi + a * b;
+  }
+}
+template <typename T>
+__device__ __forceinline__ double comp_val(T hi, T lo) {
+  if constexpr (kIsF32<T>) return ieee_add((double)hi, (double)lo);
+  else { (void)lo; return (double)hi; }
+}
+// a - b of two double-float values, rounded to T: (a_hi - b_hi) is exact for nearby float32 values
+template <typename T>
+__device__ __forceinline__ T comp_diff(T a, T al, T b, T bl) {
+  if constexpr (kIsF32<T>) {
+#pragma clang fp reassociate(off) contract(off)
+    return (a - b) + (al - bl);
+  } else {
+    (void)al; (void)bl;
+    return a - b;
+  }
+}
 
 // rudder_angle_from_sampled_route + throttle (controllers.py:306-314, 138-143, 52-62, 81-93,
 // 180-189; LOS_guidance.py:88-121).  Returns rudder, throttle and |e_ct|.
@@ -470,7 +554,7 @@ struct Ship {
 #define SIT_LOS_EXACT_INLINE __attribute__((always_inline))
 #endif
 template <typename T>
-__device__ SIT_LOS_EXACT_INLINE void los_exact(const ConstsX64& x, T n, T e, T pn, T pe, T cn, T ce, T ect_int,
+__device__ SIT_LOS_EXACT_INLINE void los_exact(const ConstsX64& x, double n, double e, T pn, T pe, T cn, T ce, double ect_int,
                                                     double& ect_abs, double& q, double& sum, bool& accept) {
   // sin / cos of the leg angle as dy / L, dx / L in IEEE float64: equal to the reference's
   // math.sin / math.cos of math.atan2 (:110-113) within an ulp or two, so e_ct is within ~1e-12 m of
@@ -480,12 +564,12 @@ __device__ SIT_LOS_EXACT_INLINE void los_exact(const ConstsX64& x, T n, T e, T p
   const double dx = ieee_sub(cn, pn), dy = ieee_sub(ce, pe);
   const double len = ieee_sqrt(ieee_sq2(dx, dy));
   const double sa = len > 0.0 ? ieee_div(dy, len) : 0.0, ca = len > 0.0 ? ieee_div(dx, len) : 1.0;
-  double ect = ieee_add(ieee_mul(-ieee_sub(n, pn), sa), ieee_mul(ieee_sub(e, pe), ca));
+  double ect = ieee_add(ieee_mul(-ieee_sub(n, (double)pn), sa), ieee_mul(ieee_sub(e, (double)pe), ca));
   ect_abs = fabs(ect);
   const double r2 = ieee_mul(x.los_r, x.los_r);
   if (ieee_mul(ect, ect) >= r2) ect = ieee_mul(0.99, x.los_r);
   q = ieee_div(ect, ieee_sqrt(ieee_sub(r2, ieee_mul(ect, ect))));
-  sum = ieee_add((double)ect_int, q);
+  sum = ieee_add(ect_int, q);
   accept = fabs(sum) <= x.windup;
 }
 
@@ -497,10 +581,20 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
                                                  bool& ect_over) {
   // next_wpt: acceptance test evaluated in IEEE float64 from the stored values (the reference's
   // decision for the same state; LOS_guidance.py:96)
-  rt.advance(ieee_sq2(ieee_sub(rt.cn, s.n), ieee_sub(rt.ce, s.e)) <= c.ra2 && rt.nw > s.k + 1, s.k);
+  // (float32: the position's double-float value; cn - n is exact in float64, then the low part)
+  double acc_dn, acc_de;
+  if constexpr (kIsF32<T>) {
+    acc_dn = ieee_sub(ieee_sub(rt.cn, s.n), (double)s.ln);
+    acc_de = ieee_sub(ieee_sub(rt.ce, s.e), (double)s.le);
+  } else {
+    acc_dn = ieee_sub(rt.cn, s.n);
+    acc_de = ieee_sub(rt.ce, s.e);
+  }
+  rt.advance(ieee_sq2(acc_dn, acc_de) <= c.ra2 && rt.nw > s.k + 1, s.k);
   const T pn = rt.pn, pe = rt.pe;
   const T alpha = rt.alpha, sa = rt.sa, ca = rt.ca;
   T q, sum;
+  T sum_lo = s.lei;
   bool accept;
   if constexpr (kIsF32<T>) {
     T ect = -(s.n - pn) * sa + (s.e - pe) * ca;
@@ -509,7 +603,7 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
     if (ect * ect >= c.los_r2) ect = c.los_clamp;         // sign lost (Q5)
     const T delta = xsqrt(c.los_r2 - ect * ect);
     q = ect / delta;
-    sum = s.ect_int + q;
+    sum = comp_add(s.ect_int, sum_lo, q);
     accept = xabs(sum) <= c.windup;
     // knife edges of the clamp (|e| = lookahead), of the navigation-failure threshold (|e| =
     // e_tolerance) and of the anti-windup limit: float32 carries ~1e-3 m of rounding in e and
@@ -518,11 +612,13 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
                                   xabs(xabs(sum) - c.windup) < T(0.02));
     if (knife) {
       double ex, qd, sd;
-      los_exact(x, s.n, s.e, pn, pe, rt.cn, rt.ce, s.ect_int, ex, qd, sd, accept);
+      los_exact(x, comp_val(s.n, s.ln), comp_val(s.e, s.le), pn, pe, rt.cn, rt.ce, comp_val(s.ect_int, s.lei), ex,
+                qd, sd, accept);
       ect_over = ex > x.e_tol;
       ect_abs = (T)ex;
       q = (T)qd;
       sum = (T)sd;
+      sum_lo = (T)ieee_sub(sd, (double)sum);
     }
   } else {
     // float64: the reference's operation order (LOS_guidance.py:112-119; no fused multiply-add,
@@ -536,20 +632,20 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
     sum = ieee_add(s.ect_int, q);
     accept = fabs(sum) <= x.windup;
   }
-  if (accept) s.ect_int = sum;
+  if (accept) { s.ect_int = sum; s.lei = sum_lo; }
   const T chi = xatan(-q - s.ect_int * c.los_ki);
   const T psi_ref = alpha + chi;
   psi_ref_out = psi_ref;
   // heading PID, error not wrapped (Q4)
   const T err = psi_ref - s.psi;
   const T derr = (err - s.hp) * c.inv_dt;
-  s.hi = s.hi + err * c.dt;
+  s.hi = comp_fma(s.hi, s.lhi, err, c.dt);
   s.hp = err;
   const T out = err * c.kp_h + derr * c.kd_h + s.hi * c.ki_h;
   rudder = xclip(-out, -c.rudder_max, c.rudder_max);
   // cascaded PI, shaft PI measures the ship speed (Q2), no saturation (Q3)
   const T e1 = v_des - s.u;
-  s.i1 = s.i1 + e1 * c.dt;
+  s.i1 = comp_fma(s.i1, s.li1, e1, c.dt);
   const T wdes = e1 * c.kp1 + s.i1 * c.ki1;
   if (simpl_of<MACH>(c)) {
     // ThrottleFromSpeedSetPointSimplifiedPropulsion.throttle (controllers.py:170-172): the ship-speed
@@ -557,7 +653,7 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
     thr = xclip(wdes, T(0), T(1.1));
   } else {
     const T e2 = wdes - s.u;
-    s.i2 = s.i2 + e2 * c.dt;
+    s.i2 = comp_fma(s.i2, s.li2, e2, c.dt);
     thr = e2 * c.kp2 + s.i2 * c.ki2;
   }
 }
@@ -566,7 +662,8 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
 // float64 arithmetic from the pre-step integrals i1, i2 and surge u; with the collision bias of
 // MSRL_Env.py:244-251 when `bias`
 template <typename T>
-__device__ __forceinline__ double throttle_exact(const ConstsX64& x, T u, T v_des, T i1, T i2, bool bias, bool simpl) {
+__device__ __forceinline__ double throttle_exact(const ConstsX64& x, T u, T v_des, double i1, double i2, bool bias,
+                                                 bool simpl) {
   const double e1 = ieee_sub(v_des, u);
   const double ii1 = ieee_add(i1, ieee_mul(e1, x.dt));
   const double wdes = ieee_dot2(e1, x.kp1, ii1, x.ki1);
@@ -691,28 +788,32 @@ __device__ __forceinline__ T power_me_kw(const Consts<T>& c, T thr) {
 // the step kernel computes it at the start of the step and issues the map lookups of that
 // position before guidance and dynamics (their LDS latency then overlaps the step's arithmetic);
 // ship_dynamics_pos stores exactly that position.
+// (ln1, le1: the post-step position's low parts, comp_add)
 template <typename T>
-__device__ __forceinline__ void euler_position(const Consts<T>& c, const Ship<T>& s, T sp, T cp, T& n1, T& e1) {
+__device__ __forceinline__ void euler_position(const Consts<T>& c, const Ship<T>& s, T sp, T cp, T& n1, T& e1, T& ln1,
+                                               T& le1) {
   const T d_n = cp * s.u - sp * s.v;
   const T d_e = sp * s.u + cp * s.v;
-  n1 = s.n + d_n * c.dt;
-  e1 = s.e + d_e * c.dt;
+  ln1 = s.ln;
+  le1 = s.le;
+  n1 = comp_fma(s.n, ln1, d_n, c.dt);
+  e1 = comp_fma(s.e, le1, d_e, c.dt);
 }
 
 template <typename T, int MACH = -1>
 __device__ __forceinline__ void ship_dynamics_pos(const Consts<T>& c, Ship<T>& s, T thr, T rudder, T sp, T cp, T n1,
-                                                  T e1);
+                                                  T e1, T ln1, T le1);
 
 template <typename T, int MACH = -1>
 __device__ __forceinline__ void ship_dynamics(const Consts<T>& c, Ship<T>& s, T thr, T rudder, T sp, T cp) {
-  T n1, e1;
-  euler_position(c, s, sp, cp, n1, e1);
-  ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
+  T n1, e1, ln1, le1;
+  euler_position(c, s, sp, cp, n1, e1, ln1, le1);
+  ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1, ln1, le1);
 }
 
 template <typename T, int MACH>
 __device__ __forceinline__ void ship_dynamics_pos(const Consts<T>& c, Ship<T>& s, T thr, T rudder, T sp, T cp, T n1,
-                                                  T e1) {
+                                                  T e1, T ln1, T le1) {
   const T u = s.u, v = s.v, r = s.r, w = s.w;
   T d_w, thrust;
   if (simpl_of<MACH>(c)) {
@@ -753,7 +854,9 @@ __device__ __forceinline__ void ship_dynamics_pos(const Consts<T>& c, Ship<T>& s
   // Euler (utils.py:50-53); the position from euler_position
   s.n = n1;
   s.e = e1;
-  s.psi = s.psi + r * c.dt;
+  s.ln = ln1;
+  s.le = le1;
+  s.psi = comp_fma(s.psi, s.lpsi, r, c.dt);
   s.u = u + (c.inv_m11 * f0) * c.dt;
   s.v = v + (c.inv_m22 * f1) * c.dt;
   s.r = r + (c.inv_m33 * f2) * c.dt;
@@ -803,7 +906,7 @@ __device__ __forceinline__ DynBase<T> dyn_base(const C& c, const Ship<T>& s, T s
 }
 template <typename T, int MACH, typename C>
 __device__ __forceinline__ void dyn_finish(const C& c, Ship<T>& s, const DynBase<T>& b, T thr, T rudder,
-                                           T n1, T e1) {
+                                           T n1, T e1, T ln1, T le1) {
   const T u = s.u, v = s.v, r = s.r, w = s.w;
   T d_w;
   if (simpl_of<MACH>(c)) {
@@ -817,7 +920,9 @@ __device__ __forceinline__ void dyn_finish(const C& c, Ship<T>& s, const DynBase
   const T f_rr = -c.c_rr * rudder * b.ur;
   s.n = n1;
   s.e = e1;
-  s.psi = s.psi + r * c.dt;
+  s.ln = ln1;
+  s.le = le1;
+  s.psi = comp_fma(s.psi, s.lpsi, r, c.dt);
   s.u = u + (c.inv_m11 * b.f0) * c.dt;
   s.v = v + (c.inv_m22 * (b.f1 + f_rv)) * c.dt;
   s.r = r + (c.inv_m33 * (b.f2 + f_rr)) * c.dt;

@@ -74,13 +74,25 @@ const FieldSpec kFields[] = {
     // iw_key_flags bit 0 = valid, bit 1 = inside; sit_load_map clears it
     {"iw_key_north", SIT_DT_REAL, kEnv},  {"iw_key_east", SIT_DT_REAL, kEnv},
     {"iw_key_flags", SIT_DT_U32, kEnv},
+    // float32 handles: the low parts of the double-float integrators (comp_add, sit_device.h): the
+    // value of north is north + north_lo, and so on.  float64 handles: zero (unused)
+    {"north_lo", SIT_DT_REAL, kShip},     {"east_lo", SIT_DT_REAL, kShip},
+    {"yaw_lo", SIT_DT_REAL, kShip},       {"ship_speed_i_lo", SIT_DT_REAL, kShip},
+    {"shaft_speed_i_lo", SIT_DT_REAL, kShip}, {"heading_i_lo", SIT_DT_REAL, kShip},
+    {"e_ct_int_lo", SIT_DT_REAL, kShip},
+    {"sampling_dist_lo", SIT_DT_REAL, kEnv},
+    {"prev_pre_north_lo", SIT_DT_REAL, kEnv}, {"prev_pre_east_lo", SIT_DT_REAL, kEnv},
 };
 constexpr int kNumFields = (int)(sizeof(kFields) / sizeof(kFields[0]));
 enum FieldId {
   F_NORTH = 0, F_LAST_PME = 14, F_K = 15, F_NW, F_TICKS, F_STOP,
   F_SAMP = 19, F_IW_E = 24, F_EP = 25, F_EVENT, F_EPISODES, F_WN, F_WE, F_LAST_OBS,
-  F_FUEL_ME, F_FUEL_EL, F_FUEL, F_LAST_LOG, F_IWK_N, F_IWK_E, F_IWK_FLAGS
+  F_FUEL_ME, F_FUEL_EL, F_FUEL, F_LAST_LOG, F_IWK_N, F_IWK_E, F_IWK_FLAGS, F_SHIP_LO, F_ENV_LO = F_SHIP_LO + 7
 };
+constexpr int kShipLo = 7;   // north, east, yaw, ship_speed_i, shaft_speed_i, heading_i, e_ct_int
+// (the episode distance, which no decision or output reads, stays a plain float32 sum)
+constexpr int kEnvLo = 3;    // sampling_dist, prev_pre_north, prev_pre_east
+static_assert(F_ENV_LO + kEnvLo == kNumFields, "state field table and ids out of sync");
 
 // per-env scenario (constant after sit_load_*), device side
 template <typename T>
@@ -92,6 +104,7 @@ struct Scen {
   const double* ab_len;   // [n_env]
   const double* ab_alpha; // [n_env]
   const T* initial_state; // [n_env][10]
+  const T* init_lo;       // [2][SIT_INIT_NF][n_env]: float32 handles, init - (float)init (double-float starts)
 };
 
 template <typename T>
@@ -112,6 +125,8 @@ struct State {
   T* last_log;            // [SIT_LOG_KEYS][n_env]: the obstacle's last logged row (log only)
   T* iwk[2];              // [n_env] each: the point of the cached IW test
   uint32_t* iwk_flags;    // [n_env]: kIwkValid | kIwkInside
+  T* ship_lo[kShipLo];    // [2 * n_env] each: the integrators' low parts (float32 handles)
+  T* env_lo[kEnvLo];      // [n_env] each
 };
 constexpr uint32_t kIwkValid = 1u, kIwkInside = 2u;
 
@@ -157,6 +172,8 @@ struct KArgs {
   int32_t n_env;
   int32_t cap;
   int32_t map_bytes;   // bytes of the map blob staged into LDS (map_stage_bytes)
+  int32_t lds_bytes;   // the launch's dynamic LDS (k_env_steps_sync; checked by the serving pass in debug builds)
+  int32_t fake_simds;  // test hook (SIT_TEST_FAKE_SIMDS): 0 = the waves' HW_ID SIMDs; else 0x100 | base-4 digits
 };
 
 // SIT_LDS_CELLS: the mixed-cell crossing records (frank, crec, clive: ~26 KB of the reference map's 57)
@@ -219,6 +236,12 @@ __device__ __forceinline__ void load_ship(const State<T>& st, int sid, Ship<T>& 
   s.ect_int = st.ship[11][sid]; s.lrpm = st.ship[12][sid]; s.lect = st.ship[13][sid];
   s.lpme = st.ship[14][sid];
   s.k = st.k[sid]; s.ticks = st.ticks[sid]; s.stop = st.stop[sid];
+  if constexpr (kIsF32<T>) {
+    s.ln = st.ship_lo[0][sid]; s.le = st.ship_lo[1][sid]; s.lpsi = st.ship_lo[2][sid];
+    s.li1 = st.ship_lo[3][sid]; s.li2 = st.ship_lo[4][sid]; s.lhi = st.ship_lo[5][sid]; s.lei = st.ship_lo[6][sid];
+  } else {
+    s.ln = s.le = s.lpsi = s.li1 = s.li2 = s.lhi = s.lei = T(0);
+  }
 }
 
 template <typename T>
@@ -229,11 +252,21 @@ __device__ __forceinline__ void store_ship(const State<T>& st, int sid, const Sh
   st.ship[11][sid] = s.ect_int; st.ship[12][sid] = s.lrpm; st.ship[13][sid] = s.lect;
   st.ship[14][sid] = s.lpme;
   st.k[sid] = s.k; st.ticks[sid] = s.ticks; st.stop[sid] = s.stop;
+  if constexpr (kIsF32<T>) {
+    st.ship_lo[0][sid] = s.ln; st.ship_lo[1][sid] = s.le; st.ship_lo[2][sid] = s.lpsi;
+    st.ship_lo[3][sid] = s.li1; st.ship_lo[4][sid] = s.li2; st.ship_lo[5][sid] = s.lhi; st.ship_lo[6][sid] = s.lei;
+  }
 }
 
 template <typename T>
 __device__ __forceinline__ T init_val(const Scen<T>& sc, int type, int f, int env, int n_env) {
   return sc.init[(type * SIT_INIT_NF + f) * n_env + env];
+}
+// the low part of a float32 handle's initial value (0 for float64)
+template <typename T>
+__device__ __forceinline__ T init_lo(const Scen<T>& sc, int type, int f, int env, int n_env) {
+  if constexpr (kIsF32<T>) return sc.init_lo[(type * SIT_INIT_NF + f) * n_env + env];
+  else return T(0);
 }
 
 // MultiShipRLEnv.reset for one ship (MSRL_Env.py:147-188): pose/velocities/time/route/LOS
@@ -247,7 +280,11 @@ __device__ __forceinline__ void reset_ship(const Scen<T>& sc, int type, int env,
   s.u = init_val(sc, type, SIT_INIT_SURGE, env, n_env);
   s.v = init_val(sc, type, SIT_INIT_SWAY, env, n_env);
   s.r = init_val(sc, type, SIT_INIT_YAW_RATE, env, n_env);
+  s.ln = init_lo(sc, type, SIT_INIT_NORTH, env, n_env);
+  s.le = init_lo(sc, type, SIT_INIT_EAST, env, n_env);
+  s.lpsi = init_lo(sc, type, SIT_INIT_YAW, env, n_env);
   s.ect_int = T(0);
+  s.lei = T(0);
   s.k = 1;
   s.ticks = 0;
   s.stop = 0;
@@ -534,6 +571,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   Route<T> rt{};
   T v_des = T(0);
   T samp = T(0), eps = T(0), ppn = T(0), ppe = T(0), iwn = T(0), iwe = T(0);
+  T samp_lo = T(0), ppn_lo = T(0), ppe_lo = T(0);   // float32: low parts (comp_add)
   // the IW's terrain test is a pure function of (iwn, iwe), which change only at sampling
   // events (or with the caller's action): cache it
   T iw_tn = T(0), iw_te = T(0);
@@ -549,7 +587,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   int32_t age0 = 0;                  // policy mode: admission rounds waited (publish_ages)
   uint32_t n_stepped = 0;
   if (MODE == kPolicy && act) {
-    const double samp0 = (double)a.st.env[0][env];
+    const double samp0 = comp_val(a.st.env[0][env], kIsF32<T> ? a.st.env_lo[0][env] : T(0));
     need = a.st.ep_step[env] == 0 || (samp0 >= a.sc.ab_len[env] && a.st.stop[n_env + env] == 0);
     ready = a.io.policy_ready[env] == SIT_POLICY_READY;
     pa = a.io.policy_action[env];
@@ -572,6 +610,10 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
       samp = a.st.env[0][env]; eps = a.st.env[1][env];
       ppn = a.st.env[2][env]; ppe = a.st.env[3][env];
       iwn = a.st.env[4][env]; iwe = a.st.env[5][env];
+      if constexpr (kIsF32<T>) {
+        samp_lo = a.st.env_lo[0][env];
+        ppn_lo = a.st.env_lo[1][env]; ppe_lo = a.st.env_lo[2][env];
+      }
       event = a.st.event[env];
       episodes = a.st.episodes[env];
       ab_len = a.sc.ab_len[env];
@@ -584,12 +626,13 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   // construction pose, route length, first leg with its geometry, and initial observation.  Only
   // with auto-reset: a launch without it (sit_step, explicit actions) skips these loads and the
   // first leg's geometry in its prologue
-  T p0[6] = {};
+  T p0[6] = {}, p0lo[3] = {};
   T lo0[6] = {};
   int nw0 = 0;
   typename Route<T>::Leg leg0{};
   if (act && __builtin_amdgcn_readfirstlane(a.io.auto_reset)) {
     for (int j = 0; j < 6; ++j) p0[j] = init_val(a.sc, type, SIT_INIT_NORTH + j, env, n_env);
+    for (int j = 0; j < 3; ++j) p0lo[j] = init_lo(a.sc, type, SIT_INIT_NORTH + j, env, n_env);
     for (int j = 0; j < lo_n; ++j) lo0[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + lo_base + j];
     nw0 = a.sc.nw0[sid];
     Route<T> r0 = rt;
@@ -655,10 +698,10 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
     if (live) xsincos(s.psi, &sp, &cp);    // heading trig of the step, off the guidance chain
     // the post-step position (a function of the pre-step state) and its map lookups, issued now:
     // their LDS latency overlaps guidance and dynamics (the predicates below use them)
-    T n1 = s.n, e1 = s.e;
+    T n1 = s.n, e1 = s.e, ln1 = s.ln, le1 = s.le;
     DistPf<T> pf;
     if (live) {
-      if (type == 0 || !s.stop) euler_position(c, s, sp, cp, n1, e1);
+      if (type == 0 || !s.stop) euler_position(c, s, sp, cp, n1, e1, ln1, le1);
       pf_cell(c, map, n1, e1, pf);
     }
     if (live) {
@@ -677,7 +720,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
           }
         } else if (MODE == kSynth) {
           init_f = (ep_step == 0);
-          sac = init_f || ((double)samp >= ab_len && !s.stop);
+          sac = init_f || (comp_val(samp, samp_lo) >= ab_len && !s.stop);
           if (sac) {                     // mode-0 action U[-1, 1] (uniform_policy.py:20-22) scaled by pi/6
             const double u01 = sampler_uniform(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event);
             act_n = u01 * 2.0 - 1.0;
@@ -719,8 +762,9 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
           if (sac) {                     // update_route: insert at index -1 (Q16)
             if (!rt.insert(iwn, iwe, s.k, a.cap)) bits |= SIT_ST_ROUTE_OVERFLOW;
             samp = T(0);
+            samp_lo = T(0);
           }
-          const T pre_n = s.n, pre_e = s.e;
+          const T pre_n = s.n, pre_e = s.e, pre_ln = s.ln, pre_le = s.le;
           T rudder, thr, psi_ref;
           guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
           if (SIT_PF_EDGES_EARLY) pf_edges(map, pf);
@@ -731,20 +775,20 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
             store_log_row<T, MACH>(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
             for (int kk = 0; kk < SIT_LOG_KEYS; ++kk) a.st.last_log[kk * row_step + env] = p_lg[kk * row_step];
           }
-          ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
+          ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1, ln1, le1);
           if (!init_f) {                 // distance between the last two stored positions
-            const T dn = pre_n - ppn, de = pre_e - ppe;
+            const T dn = comp_diff(pre_n, pre_ln, ppn, ppn_lo), de = comp_diff(pre_e, pre_le, ppe, ppe_lo);
             const T d = xsqrt(dn * dn + de * de);
             eps = eps + d;
-            samp = samp + d;
+            samp = comp_add(samp, samp_lo, d);
           }
-          ppn = pre_n; ppe = pre_e;
+          ppn = pre_n; ppe = pre_e; ppn_lo = pre_ln; ppe_lo = pre_le;
           s.ticks += 1;
         }
       } else {
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
-        const T i1_0 = s.i1, i2_0 = s.i2;   // pre-step integrals (blackout knife edge)
+        const double i1_0 = comp_val(s.i1, s.li1), i2_0 = comp_val(s.i2, s.li2);   // pre-step integrals (blackout knife edge)
         guidance_control<T, MACH>(c, cs.x, s, rt, v_des, rudder, thr, o_ect, psi_ref, ect_over);
         if (SIT_PF_EDGES_EARLY) pf_edges(map, pf);
         if (uf & kUfCollBias) {          // is_collision_imminent() on all-zero states (Q1)
@@ -766,7 +810,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
         }
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
         if (p_lg) store_log_row<T, MACH>(c, p_lg, row_step, s, thr, rudder, o_ect, psi_ref, f_me, f_el, f_tot);
-        ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1);
+        ship_dynamics_pos<T, MACH>(c, s, thr, rudder, sp, cp, n1, e1, ln1, le1);
         s.ticks += 1;
       }
 
@@ -845,7 +889,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
           stop = 1; done = true;
           bits |= SIT_ST_OBS_IW_TERMINAL;
         }
-        if (ect_over || (double)samp > samp_limit) {
+        if (ect_over || comp_val(samp, samp_lo) > samp_limit) {
           if (!stop) r_term = r_term - T(1000);
           stop = 1; done = true;
           bits |= SIT_ST_OBS_NAVIGATION;
@@ -857,7 +901,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
       x.n[type][lane] = s.n;
       x.e[type][lane] = s.e;
       x.bits[type][lane] = bits | (stop ? kStopBit : 0u) | (done ? kDoneBit : 0u) |
-                           ((MODE == kPolicy && type == 1 && (double)samp >= ab_len) ? kSampGeBit : 0u);
+                           ((MODE == kPolicy && type == 1 && comp_val(samp, samp_lo) >= ab_len) ? kSampGeBit : 0u);
       if (type == 1) { x.r_nto[lane] = r_nt; x.r_o[lane] = r_term; }
     }
     SIT_PH(3);
@@ -949,11 +993,12 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
 #endif
         // reset() (MSRL_Env.py:147-188) from the register copies
         s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];
-        s.ect_int = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
+        s.ln = p0lo[0]; s.le = p0lo[1]; s.lpsi = p0lo[2];
+        s.ect_int = T(0); s.lei = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
         rt.nw = nw0;
         rt.set_leg(leg0);
         ep_step = 0;
-        if (type == 1) { samp = T(0); eps = T(0); ++episodes; }
+        if (type == 1) { samp = T(0); eps = T(0); samp_lo = T(0); ++episodes; }
         for (int j = 0; j < 6; ++j) lo[j] = lo0[j];
         init_step_ship(c, cs.x, s, rt, v_des);
       }
@@ -992,6 +1037,10 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
       a.st.env[0][env] = samp; a.st.env[1][env] = eps;
       a.st.env[2][env] = ppn; a.st.env[3][env] = ppe;
       a.st.env[4][env] = iwn; a.st.env[5][env] = iwe;
+      if constexpr (kIsF32<T>) {
+        a.st.env_lo[0][env] = samp_lo;
+        a.st.env_lo[1][env] = ppn_lo; a.st.env_lo[2][env] = ppe_lo;
+      }
       a.st.ep_step[env] = ep_step;
       a.st.event[env] = event;
       a.st.episodes[env] = episodes;
@@ -1036,6 +1085,20 @@ __global__ __launch_bounds__(128 * kGroups, SIT_MIN_WAVES) void k_env_steps(cons
 
 #include "sit_sync.h"
 
+// this translation unit's count of k_env_steps_sync blocks whose waves shared a SIMD (sit_role_fallbacks)
+int role_fallbacks_impl(unsigned long long* out, int reset) {
+#if SIT_SIMD_ROLES
+  unsigned long long v = 0, z = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return SIT_E_HIP;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_role_fallback), sizeof(v)) != hipSuccess) return SIT_E_HIP;
+  if (reset && hipMemcpyToSymbol(HIP_SYMBOL(g_role_fallback), &z, sizeof(z)) != hipSuccess) return SIT_E_HIP;
+  *out += v;
+#else
+  (void)out; (void)reset;
+#endif
+  return SIT_OK;
+}
+
 // MultiShipRLEnv.init_step for masked envs (one thread per ship)
 template <typename T>
 __global__ __launch_bounds__(256) void k_init_step(const KArgs<T> a, const uint8_t* mask) {
@@ -1077,6 +1140,7 @@ __global__ __launch_bounds__(256) void k_reset(const KArgs<T> a, const uint8_t* 
     }
     a.st.env[0][env] = T(0);
     a.st.env[1][env] = T(0);
+    a.st.env_lo[0][env] = T(0);
     a.st.ep_step[env] = 0;
     for (int j = 0; j < SIT_OBS_DIM; ++j)
       a.st.last_obs[(size_t)j * n_env + env] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + j];
@@ -1116,7 +1180,15 @@ __global__ __launch_bounds__(256) void k_selftest_f64(int op, int n, const doubl
     case 4: r = ieee_dot2(x, y, y, x); break;
     case 5: r = sin(x); break;            // the transcendental functions the float64 path and the
     case 6: r = cos(x); break;            // knife-edge re-evaluations call (ocml): compared with
-    default: r = atan2(x, y); break;      // the reference's libm in tests/test_gpu_parity.py
+    case 7: r = atan2(x, y); break;       // the reference's libm in tests/test_gpu_parity.py
+    default: {                            // 8: k_env_steps_sync's roles for the SIMD assignment x
+      // (base 4: SIMD of wave v = digit v) and CU ticket y: role of wave v in base-4 digit v
+      const int s = (int)x, tk = (int)y;
+      int packed = 0;
+      for (int v = 0; v < 4; ++v)
+        packed |= sync_role_of(s & 3, (s >> 2) & 3, (s >> 4) & 3, (s >> 6) & 3, v, tk, SIT_SIMD_MIRROR) << (2 * v);
+      r = (double)packed;
+    }
   }
   out[i] = r;
 }
@@ -1154,11 +1226,14 @@ __global__ __launch_bounds__(256) void k_restart(const KArgs<T> a) {
     s.w = init_val(a.sc, type, SIT_INIT_SHAFT_SPEED, env, n_env);
     s.i1 = init_val(a.sc, type, SIT_INIT_SHIP_SPEED_I, env, n_env);
     s.i2 = init_val(a.sc, type, SIT_INIT_SHAFT_SPEED_I, env, n_env);
-    s.hi = T(0); s.hp = T(0); s.lrpm = T(0); s.lect = T(0); s.lpme = T(0);
+    s.li1 = init_lo(a.sc, type, SIT_INIT_SHIP_SPEED_I, env, n_env);
+    s.li2 = init_lo(a.sc, type, SIT_INIT_SHAFT_SPEED_I, env, n_env);
+    s.hi = T(0); s.hp = T(0); s.lrpm = T(0); s.lect = T(0); s.lpme = T(0); s.lhi = T(0);
     store_ship(a.st, sid, s);
     a.st.nw[sid] = nw;
   }
   for (int j = 0; j < kEnvReal; ++j) a.st.env[j][env] = T(0);
+  for (int j = 0; j < kEnvLo; ++j) a.st.env_lo[j][env] = T(0);
   a.st.ep_step[env] = 0;
   a.st.event[env] = 0;
   a.st.episodes[env] = 0;
@@ -1185,7 +1260,7 @@ struct sit_handle {
   int64_t count[kNumFields] = {};
   // scenario
   unsigned char* scen = nullptr;
-  size_t scen_init = 0, scen_end_n = 0, scen_end_e = 0, scen_nw0 = 0, scen_ab_len = 0,
+  size_t scen_init = 0, scen_init_lo = 0, scen_end_n = 0, scen_end_e = 0, scen_nw0 = 0, scen_ab_len = 0,
          scen_ab_alpha = 0, scen_initial = 0, scen_admit = 0, scen_serve = 0, scen_bytes = 0;
   // map
   unsigned char* map = nullptr;
@@ -1203,6 +1278,7 @@ struct sit_handle {
   //                            (default: staged when the launch has >= kLdsMinSteps steps)
   int kernel_classic = 0;
   int lds_map_sel = -1;
+  int fake_simds = 0;                // SIT_TEST_FAKE_SIMDS (test hook): 0x100 | base-4 SIMD assignment
   char last_kernel[96] = {};         // the step kernel of the last sit_step / sit_rollout launch
   int use_index = 0;
   double gx0 = 0, gy0 = 0, ginvx = 0, ginvy = 0, by0 = 0, binv = 0;
@@ -1407,6 +1483,8 @@ KArgs<T> make_args(const sit_handle* h) {
   a.st.last_log = fp(F_LAST_LOG);
   a.st.iwk[0] = fp(F_IWK_N); a.st.iwk[1] = fp(F_IWK_E);
   a.st.iwk_flags = reinterpret_cast<uint32_t*>(h->blob + h->off[F_IWK_FLAGS]);
+  for (int i = 0; i < kShipLo; ++i) a.st.ship_lo[i] = fp(F_SHIP_LO + i);
+  for (int i = 0; i < kEnvLo; ++i) a.st.env_lo[i] = fp(F_ENV_LO + i);
   a.sc.init = reinterpret_cast<const T*>(h->scen + h->scen_init);
   a.sc.end_n = reinterpret_cast<const T*>(h->scen + h->scen_end_n);
   a.sc.end_e = reinterpret_cast<const T*>(h->scen + h->scen_end_e);
@@ -1414,6 +1492,7 @@ KArgs<T> make_args(const sit_handle* h) {
   a.sc.ab_len = reinterpret_cast<const double*>(h->scen + h->scen_ab_len);
   a.sc.ab_alpha = reinterpret_cast<const double*>(h->scen + h->scen_ab_alpha);
   a.sc.initial_state = reinterpret_cast<const T*>(h->scen + h->scen_initial);
+  a.sc.init_lo = reinterpret_cast<const T*>(h->scen + h->scen_init_lo);
   a.map.n_poly = h->n_poly;
   a.map.n_edge = h->n_vert;
   a.map.use_index = h->use_index;
@@ -1497,11 +1576,13 @@ size_t sync_launch_lds(const sit_handle* h, const StepIO<T>& io, bool* lds_map, 
   const size_t lds = io.actor_w ? serve_lds_bytes<T>(map)
                      : policy   ? sync_lds_bytes<T, kPolicy>(map)
                      : io.action_ne ? sync_lds_bytes<T, kExplicit>(map) : sync_lds_bytes<T, kSynth>(map);
-  const size_t at = policy ? serve_lds_bytes<T>(map) : lds;
+  const size_t at_serve = (policy ? serve_lds_bytes<T>(map) : lds) + SIT_DYN_OFF;
+  const size_t at = at_serve + sizeof(Consts<T>) + 256 <= kLdsCu ? at_serve : lds + SIT_DYN_OFF;
   if (lds_map) *lds_map = sync_lds;
   if (attr) *attr = at;
-  if (h->kernel_classic || io.log || !h->use_index || at + sizeof(Consts<T>) + 256 > kLdsCu) return 0;
-  return lds;
+  // (the fit check on the LDS the launch uses: a queue-path policy launch is not refused for serving LDS)
+  if (h->kernel_classic || io.log || !h->use_index || lds + SIT_DYN_OFF + sizeof(Consts<T>) + 256 > kLdsCu) return 0;
+  return lds + SIT_DYN_OFF;
 }
 
 template <typename T>
@@ -1543,6 +1624,8 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
       h->lds_attr_sync[slot] = (int)lds_attr;
     }
     const int blocks = (h->n_env + kSyncLanes - 1) / kSyncLanes;
+    a.lds_bytes = (int32_t)(lds_sync - SIT_DYN_OFF);
+    a.fake_simds = h->fake_simds;
     void* args[] = {&a};
     HIP_TRY(h, hipLaunchKernel(kern, dim3(blocks), dim3(256), args, lds_sync, stream));
     set_kernel_name<T>(h, true, mode, sync_lds, false, mach);

@@ -12,6 +12,7 @@ int sit_launch_steps_f32(sit_handle* h, const void* io, void* stream);   // sit_
 int sit_launch_probe_f32(sit_handle* h, int n, const void* pts_ne, void* dist, uint8_t* inside, uint8_t* hull,
                          void* stream);
 int sit_launch_selftest_f32tu(int op, int n, const double* a, const double* b, double* out, void* stream);
+int sit_role_fallbacks_f32tu(unsigned long long* out, int reset);
 #ifdef SIT_DEBUG
 int sit_debug_flags_f32tu(uint32_t* out);
 #endif
@@ -68,7 +69,7 @@ int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint
 
 int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, double* out, int32_t fast_tu,
                      void* stream) {
-  if (op < 0 || op > 7 || n < 0 || (n > 0 && (!a || !b || !out))) return SIT_E_INVALID;
+  if (op < 0 || op > 8 || n < 0 || (n > 0 && (!a || !b || !out))) return SIT_E_INVALID;
   if (n == 0) return SIT_OK;
   return fast_tu ? launch_selftest_f32tu(op, n, a, b, out, stream)
                  : launch_selftest(op, n, a, b, out, (hipStream_t)stream);
@@ -143,6 +144,16 @@ int sit_debug_flags(uint32_t* flags) {
 #else
   return SIT_OK;
 #endif
+}
+int sit_role_fallbacks(uint64_t* count, int32_t reset) {
+  if (!count) return SIT_E_INVALID;
+  unsigned long long v = 0;
+  int rc = role_fallbacks_impl(&v, reset);
+#ifdef SIT_F32_TU
+  if (rc == SIT_OK) rc = sit_role_fallbacks_f32tu(&v, reset);
+#endif
+  *count = v;
+  return rc;
 }
 size_t sit_rollout_args_size(void) { return sizeof(sit_rollout_args); }
 size_t sit_params_size(void) { return sizeof(sit_params); }
@@ -239,6 +250,9 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
   // diagnostic kernel selection (read once; the launch path reads no environment)
   if (const char* sel = getenv("SIT_STEP_KERNEL")) h->kernel_classic = strcmp(sel, "classic") == 0;
   if (const char* lm = getenv("SIT_LDS_MAP")) h->lds_map_sel = (lm[0] == '0') ? 0 : (lm[0] == '1') ? 1 : -1;
+  // test hook (tests/test_gpu_placement.py): the fused step kernel's waves report SIMD digit w of this
+  // base-4 assignment (XOR the block index's low bits) instead of HW_ID, so shared-SIMD placements run
+  if (const char* fs = getenv("SIT_TEST_FAKE_SIMDS")) h->fake_simds = 0x100 | (atoi(fs) & 0xFF);
   hipError_t e = setup_device(&h->device);
   if (e != hipSuccess) { fail(nullptr, SIT_E_HIP, "hipGetDevice: %s", hipGetErrorString(e)); delete h; return SIT_E_HIP; }
   const size_t rs = real_size(h);
@@ -257,6 +271,7 @@ int sit_create(const sit_params* p, int32_t n_env, int32_t wpt_capacity, int32_t
   // scenario
   size_t so = 0;
   h->scen_init = so; so = align256(so + (size_t)2 * SIT_INIT_NF * n_env * rs);
+  h->scen_init_lo = so; so = align256(so + (size_t)2 * SIT_INIT_NF * n_env * rs);
   h->scen_end_n = so; so = align256(so + (size_t)2 * n_env * rs);
   h->scen_end_e = so; so = align256(so + (size_t)2 * n_env * rs);
   h->scen_nw0 = so; so = align256(so + (size_t)2 * n_env * 4);
@@ -638,6 +653,11 @@ int sit_load_initial(sit_handle* h, const double* init) {
   };
   auto a = conv(sc), b = conv(ist);
   HIP_TRY(h, setup_upload(h->scen + h->scen_init, a.data(), a.size()));
+  if (rs == 4) {   // float32: the low parts of the initial values (double-float starts, comp_add)
+    std::vector<float> lo(sc.size());
+    for (size_t i = 0; i < sc.size(); ++i) lo[i] = (float)(sc[i] - (double)(float)sc[i]);
+    HIP_TRY(h, setup_upload(h->scen + h->scen_init_lo, lo.data(), lo.size() * 4));
+  }
   HIP_TRY(h, setup_upload(h->scen + h->scen_initial, b.data(), b.size()));
   h->have_init = true;
   return SIT_OK;
@@ -742,10 +762,16 @@ int sit_step_host(sit_handle* h, const void* action_ne, const uint8_t* sac_updat
   return fail(h, SIT_E_STATE, "sit_step_host: no device in the host-memory test build");
 #else
   const StageLayout L = stage_layout(h);
-  if (!h->stage) {
-    HIP_TRY(h, hipHostMalloc(reinterpret_cast<void**>(&h->stage), L.bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  if (!h->stage_dev) {   // allocated into locals; published only once both calls succeeded
+    unsigned char* hp = nullptr;
+    HIP_TRY(h, hipHostMalloc(reinterpret_cast<void**>(&hp), L.bytes, hipHostMallocMapped | hipHostMallocCoherent));
     void* dp = nullptr;
-    HIP_TRY(h, hipHostGetDevicePointer(&dp, h->stage, 0));
+    const hipError_t e = hipHostGetDevicePointer(&dp, hp, 0);
+    if (e != hipSuccess || !dp) {
+      (void)hipHostFree(hp);
+      return fail(h, SIT_E_HIP, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    }
+    h->stage = hp;
     h->stage_dev = static_cast<unsigned char*>(dp);
   }
   const size_t n = (size_t)h->n_env, rs = real_size(h);

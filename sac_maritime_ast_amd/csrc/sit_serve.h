@@ -236,10 +236,19 @@ __device__ __forceinline__ void serve_pass(const float* __restrict__ w, const Se
 
 // The block's waiting envs served: every pass of kServeRows rows, then each row's head and the
 // action slot of its env.  Called by all 256 threads after barrier D (block-uniform count).
+// Debug builds check the published count against the 64 rows ServePub holds and every served env id
+// against n_env (kDbgServeCount, kDbgServeEnv: clamped, so no access leaves its table).
 template <typename T>
 __device__ __forceinline__ void serve_block(const float* __restrict__ w, bool deterministic, unsigned char* smem,
-                                            const ServePub& P, T* policy_action, unsigned long long* served) {
-  const int count = __builtin_amdgcn_readfirstlane(P.count);
+                                            const ServePub& P, T* policy_action, unsigned long long* served,
+                                            int n_env) {
+  int count = __builtin_amdgcn_readfirstlane(P.count);
+#ifdef SIT_DEBUG
+  if (count < 0 || count > kWave) {
+    SIT_DCHECK(false, kDbgServeCount);
+    count = count < 0 ? 0 : kWave;
+  }
+#endif
   if (count <= 0) return;
   ServeWork& W = *reinterpret_cast<ServeWork*>(smem);
   const int j = threadIdx.x;
@@ -251,7 +260,7 @@ __device__ __forceinline__ void serve_block(const float* __restrict__ w, bool de
   for (int row0 = 0; row0 < count; row0 += kServeRows) {
     serve_pass(w, P, W, row0, wr, b1, b2);
     if (j < kServeRows && row0 + j < count) {
-      const int e = P.env[row0 + j];
+      const int e = SIT_DCLAMP(P.env[row0 + j], n_env, kDbgServeEnv);
       policy_action[e] = (T)actor_head(W.head[2 * j], W.head[2 * j + 1], P.noise[row0 + j], deterministic);
     }
     __syncthreads();   // W reused by the next pass

@@ -30,6 +30,9 @@ extern "C" int sit_diag_read_f32(unsigned long long* out, int reset) { return di
 extern "C" int sit_diag_read_waves_f32(unsigned long long* out, int n) { return diag_read_waves_impl(out, n); }
 #endif
 
+// the float32 step kernels' blocks whose waves shared a SIMD (sit_role_fallbacks)
+int sit_role_fallbacks_f32tu(unsigned long long* out, int reset) { return role_fallbacks_impl(out, reset); }
+
 #ifdef SIT_DEBUG
 // the float32 step kernels' failed bounds checks (sit_debug_flags)
 int sit_debug_flags_f32tu(uint32_t* out) { return debug_flags_impl(out); }

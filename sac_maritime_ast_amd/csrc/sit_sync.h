@@ -152,6 +152,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   Route<T> rt{};
   T v_des = T(0);
   T samp = T(0), eps = T(0), ppn = T(0), ppe = T(0), iwn = T(0), iwe = T(0);
+  T samp_lo = T(0), ppn_lo = T(0), ppe_lo = T(0);   // float32: low parts (comp_add)
   int ep_step = 0;
   uint32_t event = 0, episodes = 0;
   double ab_len = 0.0, ab_alpha = 0.0, samp_limit = 0.0;
@@ -191,6 +192,10 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       samp = a.st.env[0][env]; eps = a.st.env[1][env];
       ppn = a.st.env[2][env]; ppe = a.st.env[3][env];
       iwn = a.st.env[4][env]; iwe = a.st.env[5][env];
+      if constexpr (kIsF32<T>) {
+        samp_lo = a.st.env_lo[0][env];
+        ppn_lo = a.st.env_lo[1][env]; ppe_lo = a.st.env_lo[2][env];
+      }
       event = a.st.event[env];
       episodes = a.st.episodes[env];
       ab_len = a.sc.ab_len[env];
@@ -212,12 +217,13 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   };
   if (TYPE == 1 && act && (MODE == kSynth || (MODE == kPolicy && ready))) draw_next();
   if (MODE == kExplicit && TYPE == 1 && act && n > 0) load_inputs(0);
-  T p0[6] = {};
+  T p0[6] = {}, p0lo[3] = {};
   int nw0 = 0;
   typename Route<T>::Leg leg0{};
   const bool auto_reset = __builtin_amdgcn_readfirstlane(a.io.auto_reset) != 0;
   if (act && auto_reset) {   // the episode start the auto reset restores (not loaded without it)
     for (int j = 0; j < 6; ++j) p0[j] = init_val(a.sc, TYPE, SIT_INIT_NORTH + j, env, n_env);
+    for (int j = 0; j < 3; ++j) p0lo[j] = init_lo(a.sc, TYPE, SIT_INIT_NORTH + j, env, n_env);
     nw0 = a.sc.nw0[sid];
     Route<T> r0 = rt;
     r0.nw = nw0;
@@ -239,11 +245,11 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     asm volatile("" : "+s"(uf));
     SyncSlot<T>& xd = X.d[it & 1];
     const T sp = sp_n, cp = cp_n;
-    T n1 = s.n, e1 = s.e;
+    T n1 = s.n, e1 = s.e, ln1 = s.ln, le1 = s.le;
     bool sac = false, init_x = false;
     double ang = 0.0, act_n = 0.0;
     if (act && !stalled) {
-      if (TYPE == 0 || !s.stop) euler_position(c, s, sp, cp, n1, e1);
+      if (TYPE == 0 || !s.stop) euler_position(c, s, sp, cp, n1, e1, ln1, le1);
       SY_MARK(10);
       if (TYPE == 1 && MODE == kExplicit) {
         // the caller's converted_action, SAC_update and init of this step (MultiShipRLEnv.step)
@@ -257,7 +263,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       } else if (TYPE == 1) {
         // a sampling event: the episode's first step, or the sampling distance reaching AB_len while
         // the obstacle ship runs (test_beds/main_ast.py:337-349 with the SURVEY 8(d) converter)
-        sac = ep_step == 0 || ((double)samp >= ab_len && !s.stop);
+        sac = ep_step == 0 || (comp_val(samp, samp_lo) >= ab_len && !s.stop);
         int32_t q = kQLive;
         if (MODE == kPolicy && sac && !ready) {
           // no action yet: the env waits for the policy for the rest of the launch (the admission
@@ -299,8 +305,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
           if (sac) {                     // update_route: insert at index -1 (Q16)
             if (!rt.insert(iwn, iwe, s.k, a.cap)) fl |= kSfOverflow;
             samp = T(0);
+            samp_lo = T(0);
           }
-          const T pre_n = s.n, pre_e = s.e;
+          const T pre_n = s.n, pre_e = s.e, pre_ln = s.ln, pre_le = s.le;
           const DynBase<T> db = dyn_base<T, MACH>(hc, s, sp, cp);   // independent of guidance: fills its latency
           T rudder, thr, psi_ref;
 #ifdef SIT_ABL_DG   // timing ablation (diagnostic builds only): no guidance / control
@@ -315,22 +322,22 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
 #ifdef SIT_ABL_DK   // timing ablation: no machinery / kinetics (the position still moves)
           s.n = n1; s.e = e1; s.psi = s.psi + T(1e-3) * rudder;
 #else
-          dyn_finish<T, MACH>(hc, s, db, thr, rudder, n1, e1);
+          dyn_finish<T, MACH>(hc, s, db, thr, rudder, n1, e1, ln1, le1);
 #endif
           xsincos(s.psi, &sp_n, &cp_n);
           SY_MARK(9);
           if (!init_f) {
-            const T dn = pre_n - ppn, de = pre_e - ppe;
+            const T dn = comp_diff(pre_n, pre_ln, ppn, ppn_lo), de = comp_diff(pre_e, pre_le, ppe, ppe_lo);
             const T d = xsqrt(dn * dn + de * de);
             eps = eps + d;
-            samp = samp + d;
+            samp = comp_add(samp, samp_lo, d);
           }
-          ppn = pre_n; ppe = pre_e;
+          ppn = pre_n; ppe = pre_e; ppn_lo = pre_ln; ppe_lo = pre_le;
           s.ticks += 1;
         }
         // is_obs_ship_navigation_failure (MSRL_env_ex.py:566-576); arrival and the map horizon are
         // the P wave's (a function of the position)
-        const bool nav = ect_over || (double)samp > samp_limit;
+        const bool nav = ect_over || comp_val(samp, samp_lo) > samp_limit;
         fl |= nav ? kSfNav : 0u;
         xd.o[0][lane] = s.n; xd.o[1][lane] = s.e; xd.o[2][lane] = s.psi; xd.o[3][lane] = o_ect;
         xd.o[4][lane] = MODE == kExplicit ? angle_or_nan(false, T(0)) : (T)act_n;
@@ -340,7 +347,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       } else {
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
-        const T i1_0 = s.i1, i2_0 = s.i2;
+        const T i1_0 = s.i1, i2_0 = s.i2, li1_0 = s.li1, li2_0 = s.li2;
         const DynBase<T> db = dyn_base<T, MACH>(hc, s, sp, cp);
 #ifdef SIT_ABL_DG
         rudder = T(0); thr = T(0.5); o_ect = T(0); psi_ref = T(0);
@@ -359,15 +366,16 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         if (uf & kUfBlackout) {
           blk = o_pme > c.blackout_kw;
           if (!kIsF32<T> || xabs(o_pme - c.blackout_kw) <= T(1e-4) * (xabs(o_pme) + T(1)))
-            blk = power_me_kw_exact(c.sg_mode, cs.x, throttle_exact(cs.x, s.u, v_des, i1_0, i2_0,
-                                                                    c.collision_bias != 0, MACH == 1))
+            blk = power_me_kw_exact(c.sg_mode, cs.x, throttle_exact(cs.x, s.u, v_des, comp_val(i1_0, li1_0),
+                                                                    comp_val(i2_0, li2_0), c.collision_bias != 0,
+                                                                    MACH == 1))
                   > cs.x.blackout;
         }
         s.lrpm = o_rpm; s.lect = o_ect; s.lpme = o_pme;
 #ifdef SIT_ABL_DK
         s.n = n1; s.e = e1; s.psi = s.psi + T(1e-3) * rudder;
 #else
-        dyn_finish<T, MACH>(hc, s, db, thr, rudder, n1, e1);
+        dyn_finish<T, MACH>(hc, s, db, thr, rudder, n1, e1, ln1, le1);
 #endif
         xsincos(s.psi, &sp_n, &cp_n);
         SY_MARK(9);
@@ -399,11 +407,12 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       if ((uf & kUfAutoReset) && env_done) {
         // reset() (MSRL_Env.py:147-188; shaft speed and every PI/PID integrator persist, Q6) + init_step()
         s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];
-        s.ect_int = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
+        s.ln = p0lo[0]; s.le = p0lo[1]; s.lpsi = p0lo[2];
+        s.ect_int = T(0); s.lei = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
         rt.nw = nw0;
         rt.set_leg(leg0);
         ep_step = 0;
-        if (TYPE == 1) { samp = T(0); eps = T(0); ++episodes; }
+        if (TYPE == 1) { samp = T(0); eps = T(0); samp_lo = T(0); ++episodes; }
         init_step_ship(c, cs.x, s, rt, v_des);
         xsincos(s.psi, &sp_n, &cp_n);
       }
@@ -422,6 +431,10 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       a.st.env[0][env] = samp; a.st.env[1][env] = eps;
       a.st.env[2][env] = ppn; a.st.env[3][env] = ppe;
       a.st.env[4][env] = iwn; a.st.env[5][env] = iwe;
+      if constexpr (kIsF32<T>) {
+        a.st.env_lo[0][env] = samp_lo;
+        a.st.env_lo[1][env] = ppn_lo; a.st.env_lo[2][env] = ppe_lo;
+      }
       a.st.ep_step[env] = ep_step;
       a.st.event[env] = event;
       a.st.episodes[env] = episodes;
@@ -779,22 +792,32 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
 #else
 #define SIT_SYNC_OCC
 #endif
-// Roles by SIMD (fused launches): a block's four waves sit on four different SIMDs and a CU holds two
-// blocks (i and i + 256), so fixed roles by wave index left a quarter of the SIMDs with two D waves and
-// a quarter with two P waves.  Each wave takes its role from the SIMD it runs on (HW_ID), mirrored for
-// the second block of its CU (a per-CU ticket, one atomic per block while the map stages), so every SIMD
-// holds one D and one P wave — which the issue priorities above then order.  Measured C3 +3.3 % with the
-// priorities (without them, round 3: -0.3 %), C5 unchanged.  Single-step launches (map through the
-// caches, nothing staged to hide the ticket's round trip behind) keep the fixed order.
-#ifndef SIT_SIMD_ROLES
-#define SIT_SIMD_ROLES 1
+// Roles by SIMD (fused launches): round 3 observed a block's four waves on four different SIMDs and a
+// CU holding two blocks (i and i + 256), so fixed roles by wave index left a quarter of the SIMDs with
+// two D waves and a quarter with two P waves.  Each wave takes its role from the SIMD it runs on
+// (HW_ID), mirrored for the second block of its CU (a per-CU ticket, one atomic per block while the
+// map stages), so every SIMD holds one D and one P wave — which the issue priorities above then order.
+// Measured C3 +3.3 % with the priorities (without them, round 3: -0.3 %), C5 unchanged.  Single-step
+// launches (map through the caches, nothing staged to hide the ticket's round trip behind) keep the
+// fixed order.
+// Placement independence: the hardware does not guarantee that placement (another kernel on the CU,
+// RCCL beside the step at N > 1, a second stream group can change it).  So the role is not the SIMD
+// itself but the rank of the wave's (SIMD, wave index) among the block's four (sync_role_of,
+// sit_device.h): always a permutation of D0, D1, P0, P1 — every role runs exactly once per block,
+// whatever the placement — and equal to the SIMD when the four differ.  Blocks whose waves share a
+// SIMD are counted (g_role_fallback, sit_role_fallbacks): results are unaffected, only the priorities'
+// pairing.  (The per-CU ticket is shared by concurrent launches; that, too, only affects speed.)
+#ifndef SIT_DYN_OFF
+#define SIT_DYN_OFF 0
 #endif
 #if SIT_SIMD_ROLES
 __device__ int g_cu_ticket[2048];
+__device__ unsigned long long g_role_fallback;   // blocks whose four waves did not sit on four SIMDs
 #endif
 template <typename T, int MODE, int MACH, bool LDSMAP>
 __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs<T> a) {
-  extern __shared__ __align__(16) unsigned char smem[];
+  extern __shared__ __align__(16) unsigned char smem_dyn[];
+  unsigned char* const smem = smem_dyn + SIT_DYN_OFF;   // (SIT_DYN_OFF: experiment, the LDS layout's offset)
   __shared__ Consts<T> cs;
 #ifdef SIT_DIAG_SYNC
   const unsigned long long sy_k0 = __builtin_amdgcn_s_memtime();
@@ -805,25 +828,35 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #if SIT_SIMD_ROLES
   __shared__ int s_tk;
-  if (LDSMAP && threadIdx.x == 0) {
+  __shared__ int s_simd[4];   // the SIMD of each wave of the block (HW_ID[5:4])
+  if (LDSMAP) {
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);     // HW_REG_HW_ID
-    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);   // HW_REG_XCC_ID
-    const unsigned key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) & 2047;
-    s_tk = atomicAdd(&g_cu_ticket[key], 1) & 1;
+    const int fk = __builtin_amdgcn_readfirstlane(a.fake_simds);
+    if ((threadIdx.x & (kWave - 1)) == 0)
+      s_simd[w] = fk ? (((fk >> (2 * w)) ^ (int)blockIdx.x) & 3) : (int)((hw >> 4) & 3);
+    if (threadIdx.x == 0) {
+      const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);   // HW_REG_XCC_ID
+      const unsigned key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) & 2047;
+      s_tk = atomicAdd(&g_cu_ticket[key], 1) & 1;
+    }
   }
 #endif
   const int lane = threadIdx.x & (kWave - 1);
   const int env = blockIdx.x * kSyncLanes + lane;
   const bool act = lane < kSyncLanes && env < a.n_env;
   SyncShared<T>& X = *reinterpret_cast<SyncShared<T>*>(smem + (LDSMAP ? (((size_t)a.map_bytes + 255) & ~size_t(255)) : 0));
-  __syncthreads();   // constants copied, map staged
+  __syncthreads();   // constants copied, map staged, SIMDs published
 #if SIT_SIMD_ROLES
-  const int simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) >> 4) & 3);
-#ifndef SIT_SIMD_MIRROR
-#define SIT_SIMD_MIRROR 2   // the second block's roles: simd ^ 2 pairs (D0, P0), (D1, P1); ^ 3 pairs (D0, P1), (D1, P0)
-#endif
-  const int role = LDSMAP ? __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readfirstlane(s_tk) ? (simd ^ SIT_SIMD_MIRROR) : simd)
-                          : ((blockIdx.x & 1) == 0 ? w : (w ^ 2));
+  int role;
+  if (LDSMAP) {
+    const int s0 = __builtin_amdgcn_readfirstlane(s_simd[0]), s1 = __builtin_amdgcn_readfirstlane(s_simd[1]);
+    const int s2 = __builtin_amdgcn_readfirstlane(s_simd[2]), s3 = __builtin_amdgcn_readfirstlane(s_simd[3]);
+    role = __builtin_amdgcn_readfirstlane(
+        sync_role_of(s0, s1, s2, s3, w, __builtin_amdgcn_readfirstlane(s_tk), SIT_SIMD_MIRROR));
+    if (threadIdx.x == 0 && !sync_simds_distinct(s0, s1, s2, s3)) atomicAdd(&g_role_fallback, 1ull);
+  } else {
+    role = (blockIdx.x & 1) == 0 ? w : (w ^ 2);
+  }
 #else
   const int role = (blockIdx.x & 1) == 0 ? w : (w ^ 2);
 #endif
@@ -860,7 +893,13 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
     const unsigned long long sy_s0 = __builtin_amdgcn_s_memtime();
 #endif
     __syncthreads();   // D: the block's waiting envs published; the map and exchange slots are dead
-    serve_block<T>(a.io.actor_w, a.io.actor_det != 0, smem, *pub, a.io.policy_action, a.io.actor_served);
+#ifdef SIT_DEBUG   // the serving LDS (ServeWork at 0, ServePub after it) inside the launch's dynamic LDS
+    if (serve_lds_bytes<T>(LDSMAP ? (size_t)a.map_bytes : 0) > (size_t)a.lds_bytes) {
+      if (threadIdx.x == 0) SIT_DCHECK(false, kDbgServeCount);
+      return;
+    }
+#endif
+    serve_block<T>(a.io.actor_w, a.io.actor_det != 0, smem, *pub, a.io.policy_action, a.io.actor_served, a.n_env);
 #ifdef SIT_DIAG_SYNC   // slot 14: the wait at barrier D and the serving (per launch)
     if (lane == 0) atomicAdd(&g_sit_diag[role >> 1][(role & 1) * 16 + 14], __builtin_amdgcn_s_memtime() - sy_s0);
 #endif

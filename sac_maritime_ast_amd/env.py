@@ -27,6 +27,14 @@ def _ptr(t):
     return None if t is None else c_void_p(t.data_ptr())
 
 
+# float32 handles keep these fields as double-float values (hi + lo; csrc/sit_device.h comp_add): the
+# reference integrates them in float64, and a float32 running sum loses up to half an ulp a step
+LO_FIELDS = {"north": "north_lo", "east": "east_lo", "yaw": "yaw_lo", "ship_speed_i": "ship_speed_i_lo",
+             "shaft_speed_i": "shaft_speed_i_lo", "heading_i": "heading_i_lo", "e_ct_int": "e_ct_int_lo",
+             "sampling_dist": "sampling_dist_lo", "prev_pre_north": "prev_pre_north_lo",
+             "prev_pre_east": "prev_pre_east_lo"}
+
+
 class VecMultiShipRLEnv:
     """N two-ship environments resident in HBM.
 
@@ -273,19 +281,33 @@ class VecMultiShipRLEnv:
             views[name] = v
         return views
 
-    def get_state(self):
+    def get_state(self, combined: bool = False):
         """Named tensors (copies): ship fields [2, n_env], env fields [n_env], route tables
-        [2, cap, n_env].  Unsigned fields are returned as int32."""
-        return self._views(self.state_blob())
+        [2, cap, n_env].  Unsigned fields are returned as int32.  A float32 handle holds the fields of
+        LO_FIELDS as hi + lo (the `<name>_lo` fields); combined=True returns them as float64 values
+        hi + lo, without the `_lo` fields."""
+        st = self._views(self.state_blob())
+        if combined:
+            for hi, lo in LO_FIELDS.items():
+                st[hi] = st[hi].to(torch.float64) + st.pop(lo).to(torch.float64)
+        return st
 
     def set_state(self, state: dict):
+        """Writes the given fields.  A field of LO_FIELDS given without its `_lo` part gets it from the
+        value (float32 handles: the value's float64 rounding residual, so a float64 state is held
+        exactly as hi + lo; float64 handles: 0)."""
         blob = self.state_blob()
         views = self._views(blob)
         for k, v in state.items():
             if k not in views:
                 continue
-            views[k].copy_(torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v)
-                           .to(dtype=views[k].dtype, device=self.device).reshape(views[k].shape))
+            t = torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v).reshape(views[k].shape)
+            views[k].copy_(t.to(dtype=views[k].dtype, device=self.device))
+            lo = LO_FIELDS.get(k)
+            if lo is not None and lo in views and lo not in state:
+                x = t.to(dtype=torch.float64, device=self.device)
+                views[lo].copy_((x - x.to(torch.float32).to(torch.float64)).to(views[lo].dtype)
+                                if self.precision == 32 else torch.zeros_like(views[lo]))
         self.load_state_blob(blob)
 
     def close(self):

@@ -194,6 +194,88 @@ class AsyncTransitionGather:
         return self.n_dropped
 
 
+class TrajectoryGather:
+    """Strided trajectory rows of every rank to the learner rank (the RCCL gather of
+    trajectory chunks), for consumers that need whole trajectories on one rank.
+
+    A launch of K steps writes rows [K, n_env, ...] per rank (next_state, reward, done, status); every
+    `stride`-th row (rows 0, stride, 2 stride, ...) of each rank is copied into a send buffer on the
+    collective stream, behind the launch, and sent point-to-point to the learner, which receives
+    rank r's rows into slot r.  Sizes are fixed by (K, stride, n_env), so no count exchange is needed.
+    The launch stream waits only for the copy (``start``), not for the transfer; ``wait`` joins the
+    transfer.  Why strided: a C3 launch writes 65 B per env-step, 2.1 MB per step per rank; all rows of 7
+    ranks into one GPU would need ~7 TB/s, while the transitions the SAC learner consumes are gathered
+    whole (AsyncTransitionGather)."""
+
+    FIELDS = ("next_state", "reward", "done", "status")
+
+    def __init__(self, k: int, n_env: int, stride: int, dtype, device, world: int, group=None, dst: int = 0):
+        if stride < 1 or k < 1:
+            raise ValueError("need k >= 1 and stride >= 1")
+        self.k, self.n_env, self.stride, self.world, self.group, self.dst = k, n_env, stride, world, group, dst
+        self.rank = dist.get_rank(group) if world > 1 else 0
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.rows = -(-k // stride)
+        shapes = {"next_state": ((self.rows, n_env, 10), dtype), "reward": ((self.rows, n_env), dtype),
+                  "done": ((self.rows, n_env), torch.uint8), "status": ((self.rows, n_env), torch.int32)}
+        self.send = {f: torch.empty(shp, dtype=dt, device=device) for f, (shp, dt) in shapes.items()}
+        nrecv = world if self.rank == dst else 0
+        self.recv = {f: [torch.empty(shp, dtype=dt, device=device) for _ in range(nrecv)]
+                     for f, (shp, dt) in shapes.items()}
+        self.stream = torch.cuda.Stream(device=self.device) if self.cuda else None
+        self.work = []
+        self.bytes_moved = 0     # bytes received by the learner from the other ranks
+
+    def start(self, out: dict):
+        """Queue the strided copy of `out`'s rows (behind the launch that wrote them) and their transfer
+        to the learner.  The caller's stream waits for the copy only: the next launch may then reuse
+        `out` while the rows travel."""
+        self.wait()
+        cur = torch.cuda.current_stream(self.device) if self.cuda else None
+        if self.cuda:
+            self.stream.wait_stream(cur)
+        ctx = torch.cuda.stream(self.stream) if self.cuda else _Null()
+        with ctx:
+            for f in self.FIELDS:
+                self.send[f].copy_(out[f][::self.stride])
+            if self.cuda:
+                copied = torch.cuda.Event()
+                copied.record(self.stream)
+            ops = []
+            if self.world > 1:
+                if self.rank == self.dst:
+                    for r in range(self.world):
+                        if r != self.dst:
+                            ops += [dist.P2POp(dist.irecv, self.recv[f][r], r, self.group) for f in self.FIELDS]
+                else:
+                    ops += [dist.P2POp(dist.isend, self.send[f], self.dst, self.group) for f in self.FIELDS]
+            self.work = dist.batch_isend_irecv(ops) if ops else []
+            if self.rank == self.dst:
+                for f in self.FIELDS:
+                    if self.world > 1:
+                        self.recv[f][self.rank].copy_(self.send[f])
+                if self.world > 1:
+                    self.bytes_moved += (self.world - 1) * sum(t.numel() * t.element_size() for t in self.send.values())
+        if self.cuda:
+            cur.wait_event(copied)
+
+    def wait(self):
+        for w in self.work:
+            w.wait()
+        self.work = []
+        if self.cuda:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+    def gathered(self, field: str):
+        """[world, rows, n_env, ...] of the last started launch (learner rank, after wait())."""
+        if self.rank != self.dst:
+            raise RuntimeError("only the learner rank holds the gathered rows")
+        if self.world == 1:
+            return self.send[field].unsqueeze(0)
+        return torch.stack(self.recv[field])
+
+
 class _Null:
     def __enter__(self):
         return self

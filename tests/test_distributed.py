@@ -140,3 +140,42 @@ def test_async_transition_gather_two_ranks(tmp_path):
     path = str(tmp_path / "result_async.txt")
     mp.spawn(_async_worker, args=(2, _free_port(), path), nprocs=2, join=True)
     assert open(path).read() == "ok"
+
+
+def _traj_worker(rank, world, port, result_path):
+    """TrajectoryGather: every stride-th row of each rank's launch rows arrives on the learner in
+    rank order (the oracle's sharded rollouts: rank r's rows are global envs [r n, (r + 1) n)), and the
+    gathered rows equal the strided rows of one big run."""
+    from sac_maritime_ast_amd.shard import TrajectoryGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        off = shard_offset(rank, N_PER_RANK)
+        r = _rollout(N_PER_RANK, off)
+        out = {"next_state": torch.from_numpy(r["next_state"]), "reward": torch.from_numpy(r["reward"]),
+               "done": torch.from_numpy(r["done"].astype(np.uint8)),
+               "status": torch.from_numpy(r["status"].astype(np.int32))}
+        stride = 7
+        g = TrajectoryGather(STEPS, N_PER_RANK, stride, torch.float64, "cpu", world)
+        g.start(out)
+        g.wait()
+        if rank == 0:
+            full = _rollout(world * N_PER_RANK, 0)
+            ns = g.gathered("next_state")                       # [world, rows, n, 10]
+            assert ns.shape == (world, -(-STEPS // stride), N_PER_RANK, 10)
+            got = torch.cat(list(ns), dim=1).numpy()            # rank order = global env order
+            np.testing.assert_allclose(got, full["next_state"][::stride], rtol=1e-12, atol=1e-9)
+            st = torch.cat(list(g.gathered("status")), dim=1).numpy()
+            assert np.array_equal(st.astype(np.int64) & 0xFFFFFFFF, full["status"][::stride].astype(np.int64))
+            assert g.bytes_moved == sum(t.numel() * t.element_size() for t in g.send.values())
+            with open(result_path, "w") as f:
+                f.write("ok")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_trajectory_gather_two_ranks(tmp_path):
+    path = str(tmp_path / "result_traj.txt")
+    mp.spawn(_traj_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    assert open(path).read() == "ok"

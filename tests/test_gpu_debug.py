@@ -1,7 +1,8 @@
 """The bounds-checked debug variant of the library (libsit_debug.so, -DSIT_DEBUG; SURVEY §5 "bounds
 asserts in a debug kernel variant"): every table index the step kernels compute is checked before
 use (route rows, waypoint index, route length, spatial-index entries, edge ids, class-grid words,
-mixed-cell records).  The workload of every kernel variant runs under it with no check failing; a
+mixed-cell records), and the in-kernel serving pass its published row count, served env ids and
+LDS extents.  The workload of every kernel variant runs under it with no check failing; a
 deliberately corrupted waypoint index and route length are reported (and clamped, so nothing is read
 out of bounds).  The debug library runs in a child process (SIT_LIBRARY) so that this test session
 keeps the release library."""
@@ -54,6 +55,18 @@ sm = PolicySampler(env, GaussianPolicy().to("cuda:0"), chunk=64, request_capacit
 for _ in range(30):
     sm.launch()
 res["f32_policy"] = read()
+# policy mode with in-kernel serving (csrc/sit_serve.h: published rows, served env ids, the serving LDS)
+# on ragged populations (a partial last block), float32 and float64
+for prec, n_r in ((32, 4096 - 37), (64, 512 - 5)):
+    er = VecMultiShipRLEnv(scenario=make_scenario(n_r, cap=48), precision=prec, device="cuda:0")
+    er.reset(); er.init_step()
+    sk = PolicySampler(er, GaussianPolicy().to("cuda:0"), chunk=64, serve="kernel")
+    for _ in range(30):
+        sk.launch()
+    torch.cuda.synchronize()
+    res[f"f{prec}_policy_serve"] = read()
+    res[f"f{prec}_policy_serve_kernel"] = er.lib.sit_step_kernel(er.handle).decode()
+    res[f"f{prec}_served"] = int(sk.served.item())
 # corrupted state: the checks fire and clamp (no out-of-bounds access)
 st = env.get_state()
 st["next_wpt"][1, 0] = 999
@@ -79,7 +92,10 @@ def test_debug_variant_checks_every_kernel():
     res = json.loads(p.stdout.strip().splitlines()[-1])
     print("debug variant:", res)
     assert res["debug_build"] == 1
-    for k in ("f32_sync", "f64_log_step_probe", "f32_policy"):
+    for k in ("f32_sync", "f64_log_step_probe", "f32_policy", "f32_policy_serve", "f64_policy_serve"):
         assert res[k] == 0, f"{k}: bounds checks failed: {res[k]:#x}"
+    for prec in (32, 64):   # the serving pass ran (inside the sync kernel) and served envs
+        assert "k_env_steps_sync" in res[f"f{prec}_policy_serve_kernel"], res
+        assert res[f"f{prec}_served"] > 0, res
     assert res["bad_waypoint"] & (1 << 1), res          # kDbgWaypoint
     assert res["bad_route_len"] & (1 << 2), res         # kDbgRouteLen

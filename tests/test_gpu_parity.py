@@ -491,8 +491,8 @@ def test_f32_free_running_within_storage_bound():
     state STORAGE alone costs.  Per env the runs are compared until the first step whose discrete
     outcome differs (done, status, sampling event, waypoint index, route length, stop flags, episode
     step, sampler counter).  Gated: before divergence the next_state deviation (per-field floors) is
-    within SURVEY §8(d)'s storage bound 2.5e-5; the float32 arithmetic adds at most 50 % to what
-    storage alone costs; at most 2 % of envs diverge.  Every divergence is attributed
+    within north_star's 1e-5 and below what plain float32 storage alone costs (the float32 handle keeps
+    its integrators as double-float values); at most 0.25 % of envs diverge.  Every divergence is attributed
     (f32_drift.measure(attribute=True)): re-run in float64 from the float32 run's own pre-step state,
     the step takes the float32 decision (the state's float32 drift decided it), or, where it takes the
     float64 one, the flip is a hull-in-terrain decision whose exact (float64) predicate at the stored
@@ -519,9 +519,12 @@ def test_f32_free_running_within_storage_bound():
           f"{f32['earliest_divergence_step']}), next_state max {f32['next_state_max']:.2e} p99 "
           f"{f32['next_state_p99']:.2e}; float32 storage alone: {s32['envs_diverged']} diverged, max "
           f"{s32['next_state_max']:.2e}")
-    assert f32["next_state_max"] <= 2.5e-5
-    assert f32["next_state_max"] <= 1.5 * s32["next_state_max"] + 1e-6
-    assert f32["envs_diverged"] <= 0.02 * 4096
+    # north_star's 1e-5 before any decision moves; the double-float integrators (csrc/sit_device.h
+    # comp_add) took float32 below what float32 state storage alone costs (round 4, plain float32 sums:
+    # 38 envs diverged, max 9.95e-6; round 5: 9 envs, max 3.5e-6, profiles/r05_f32_flip_attribution.json)
+    assert f32["next_state_max"] <= 1e-5
+    assert f32["next_state_max"] <= s32["next_state_max"]
+    assert f32["envs_diverged"] <= 0.0025 * 4096
 
 
 # ------------------------------------------------------------------------------------------

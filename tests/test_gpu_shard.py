@@ -60,3 +60,28 @@ def test_async_gather_device_branch_world1(slots):
     assert total > n_launch * n_env * chunk // 600     # ~1 record per 390 env-steps
     assert ga.gathered == total and ga.dropped() == 0
     assert ga.launches == n_launch
+
+
+def test_trajectory_gather_device_branch_world1():
+    """TrajectoryGather on the GPU (world 1: the learner keeps its own strided rows): the collective
+    stream's strided copy behind each launch equals the launch's rows, and the next launch reusing the
+    same output buffers does not disturb the gathered copy (the launch stream waits for the copy)."""
+    from sac_maritime_ast_amd.shard import TrajectoryGather
+    n, k, stride = 2048, 200, 9
+    env = VecMultiShipRLEnv(scenario=make_scenario(n, cap=48), precision=32, device="cuda:0")
+    env.reset()
+    env.init_step()
+    g = TrajectoryGather(k, n, stride, env.dtype, "cuda:0", 1)
+    out = {}
+    for it in range(3):
+        env.rollout(k, seed=5, out=out)
+        want = {f: out[f][::stride].clone() for f in TrajectoryGather.FIELDS}
+        g.start(out)
+        env.rollout(k, seed=6, out=out)            # overwrites `out` while the gather's copy is queued
+        g.wait()
+        for f in TrajectoryGather.FIELDS:
+            got = g.gathered(f)[0]
+            if got.is_floating_point():
+                assert torch.equal(got.view(torch.int32), want[f].view(torch.int32)), (it, f)
+            else:
+                assert torch.equal(got, want[f]), (it, f)

@@ -19,7 +19,9 @@ benchmark times; the obstacle slot steps its own route and is not compared.
     on the same float32 state: <= 1e-5 relative, waypoint index identical — the knife edges
     included (the kernel re-takes those decisions in float64, sit_device.h guidance_control).
 """
+import json
 import math
+import os
 
 import numpy as np
 import pytest
@@ -191,8 +193,33 @@ def test_f64_sim_teacher_forced_vs_reference(case):
     if knife.any():
         print(f"{name} bias={bias}: {int(knife.sum())} of {len(rows)} cases on a float64 libm-ulp knife edge of the "
               f"LOS clamp, {int((off & knife).sum())} of them decided the other way")
+    _knife_record(f"{name}[{case}]", int(knife.sum()), int((off & knife).sum()))
     bad = np.nonzero(off & ~knife)[0]
     assert bad.size == 0, f"{name} bias={bias}: cases {rows[bad[:5]]} off by {worst[bad[:5]]}"
+
+
+KNIFE_PIN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "knife_edge_counts.json")
+
+
+def _knife_record(key, n_knife, n_other):
+    """The libm knife edges per fixture, persisted and pinned: how many cases sit on a float64 libm-ulp
+    knife edge of the LOS clamp (a function of the fixture: asserted) and how many of them the device's
+    float64 libm decides the other way (a property of the device math library: pinned to the committed
+    count in tests/golden/knife_edge_counts.json, recorded from the GPU run in
+    profiles/r05_knife_edges.json; a change of libm shows up here).  SIT_TEST_RECORD_DIR: also write the
+    observed counts there."""
+    pin = json.load(open(KNIFE_PIN)) if os.path.exists(KNIFE_PIN) else {}
+    rec_dir = os.environ.get("SIT_TEST_RECORD_DIR")
+    if rec_dir:
+        os.makedirs(rec_dir, exist_ok=True)
+        path = os.path.join(rec_dir, "knife_edges.json")
+        cur = json.load(open(path)) if os.path.exists(path) else {}
+        cur[key] = {"knife_edge_cases": n_knife, "decided_other_way": n_other}
+        with open(path, "w") as f:
+            json.dump(cur, f, indent=1, sort_keys=True)
+    if key in pin:
+        assert n_knife == pin[key]["knife_edge_cases"], (key, n_knife, pin[key])
+        assert n_other <= pin[key]["decided_other_way"], (key, n_other, pin[key])
 
 
 @pytest.mark.parametrize("case", range(2 + len(TRAJ)))

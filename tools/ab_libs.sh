@@ -7,7 +7,7 @@ rounds=$1; shift
 for r in $(seq 1 $rounds); do
   for lib in "$@"; do
     n=$(basename $lib .so)
-    SIT_LIBRARY=$lib timeout -k 10 150 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} \
+    SIT_LIBRARY=$lib timeout -k 10 150 python bench.py --no-cpu-baseline --no-extra-lines ${BENCH_ARGS:-} \
       > gpurun_out/ab/${n}_$r.json 2> gpurun_out/ab/${n}_$r.err || { echo "$n failed"; tail -3 gpurun_out/ab/${n}_$r.err; exit 1; }
     python -c "
 import json; d=json.loads(open('gpurun_out/ab/${n}_$r.json').read().strip().splitlines()[-1])

@@ -34,7 +34,8 @@ INTS = ("next_wpt", "n_wpt", "stop", "ep_step", "event")
 
 
 def state(env):
-    return {k: v.cpu().numpy() for k, v in env.get_state().items()}
+    """The state with the float32 handle's double-float fields as their float64 values hi + lo."""
+    return {k: v.cpu().numpy() for k, v in env.get_state(combined=True).items()}
 
 
 def rel(a, b, floor):

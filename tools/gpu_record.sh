@@ -12,7 +12,7 @@ C5="--mode policy --chunk 64 --groups 1 --steps 8192 --warmup 16384"
 tools/gpu_steps.sh \
  $T/smoke 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" --- \
  $T/bench 400 python3 -u bench.py --- \
- $T/prof_c3 400 rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --- \
+ $T/prof_c3 400 rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extra-lines --- \
  $T/prof_step 300 rocprofv3 --kernel-trace --stats -d $O/prof_step -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mode step --no-c5 --steps 2000 --warmup 200 --- \
  $T/pmc_c3 900 bash tools/pmc.sh $O/pmc_c3 --no-c5 --- \
  $T/pmc_c5 900 bash tools/pmc.sh $O/pmc_c5 $C5

@@ -5,7 +5,7 @@ set -u
 out=$1
 shift
 mkdir -p $out
-BENCH="python3 bench.py --no-cpu-baseline $*"
+BENCH="python3 bench.py --no-cpu-baseline --no-extra-lines $*"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
