@@ -452,7 +452,11 @@ struct Route {
     fix = false;
   }
   __device__ __forceinline__ void fixup(int k) {
+#ifdef SIT_ABL_FIXUP   // timing ablation (diagnostic builds only, results wrong): no route-table read
+    if (fix) { nn = cn + T(100); ne = ce + T(100); leg_geom(cn, ce, nn, ne, alpha_n, sa_n, ca_n); fix = false; (void)k; }
+#else
     if (fix) { load_next(k); fix = false; }
+#endif
   }
   // update_route: insert (in_, ie) at index -1 (controllers.py:298-303); false on overflow
   __device__ __forceinline__ bool insert(T in_, T ie, int k, int cap) {
@@ -499,9 +503,15 @@ struct Ship {
 // (compensated summation, Fast2Sum: |hi| >= |inc| for all but zero crossings, where the terms are
 // small): hi stays the float32-rounded running sum and the error no longer accumulates.  The
 // decisions read hi + lo in float64 (comp_val).  float64 handles: the plain sum.
+#ifndef SIT_COMP
+#define SIT_COMP 1   // (0: experiment only, plain float32 sums, to price the compensation)
+#endif
+template <typename T>
+constexpr bool kComp = kIsF32<T> && SIT_COMP != 0;
+
 template <typename T>
 __device__ __forceinline__ T comp_add(T hi, T& lo, T inc) {
-  if constexpr (kIsF32<T>) {
+  if constexpr (kComp<T>) {
 #pragma clang fp reassociate(off) contract(off)
     const T y = inc + lo;
     const T t = hi + y;
@@ -512,11 +522,12 @@ __device__ __forceinline__ T comp_add(T hi, T& lo, T inc) {
     return hi + inc;
   }
 }
-// hi + a * b as comp_add, the product fused into the low part's update (one rounding, one extra
-// dependent instruction on the integrator's chain: t = hi + fma(a, b, lo))
+// hi + a * b as comp_add, the product fused into the low part's update: y = fma(a, b, lo), t = hi + y
+// (one dependent instruction more on the integrator's chain than the plain fma; folding lo / dt into the
+// factor instead kept the chain but measured C3 -2 %: more registers live across guidance)
 template <typename T>
 __device__ __forceinline__ T comp_fma(T hi, T& lo, T a, T b) {
-  if constexpr (kIsF32<T>) {
+  if constexpr (kComp<T>) {
 #pragma clang fp reassociate(off) contract(off)
     const T y = __builtin_fmaf(a, b, lo);
     const T t = hi + y;
@@ -529,13 +540,13 @@ __device__ __forceinline__ T comp_fma(T hi, T& lo, T a, T b) {
 }
 template <typename T>
 __device__ __forceinline__ double comp_val(T hi, T lo) {
-  if constexpr (kIsF32<T>) return ieee_add((double)hi, (double)lo);
+  if constexpr (kComp<T>) return ieee_add((double)hi, (double)lo);
   else { (void)lo; return (double)hi; }
 }
 // a - b of two double-float values, rounded to T: (a_hi - b_hi) is exact for nearby float32 values
 template <typename T>
 __device__ __forceinline__ T comp_diff(T a, T al, T b, T bl) {
-  if constexpr (kIsF32<T>) {
+  if constexpr (kComp<T>) {
 #pragma clang fp reassociate(off) contract(off)
     return (a - b) + (al - bl);
   } else {
@@ -583,7 +594,7 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
   // decision for the same state; LOS_guidance.py:96)
   // (float32: the position's double-float value; cn - n is exact in float64, then the low part)
   double acc_dn, acc_de;
-  if constexpr (kIsF32<T>) {
+  if constexpr (kComp<T>) {
     acc_dn = ieee_sub(ieee_sub(rt.cn, s.n), (double)s.ln);
     acc_de = ieee_sub(ieee_sub(rt.ce, s.e), (double)s.le);
   } else {

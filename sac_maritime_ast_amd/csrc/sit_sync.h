@@ -287,7 +287,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       xd.q[lane] = kQStalled;
     }
     SY_MARK(0);
+#ifndef SIT_ABL_NO_A   // timing ablation (diagnostic builds only, results wrong): no barrier A
     __syncthreads();   // A: positions (and the IW, and in policy mode the step's decision) published
+#endif
     SY_MARK(1);
     if (MODE == kPolicy && TYPE == 0 && act && !stalled) stalled = xd.q[lane] != kQLive;
     if (act && !stalled) {
@@ -636,7 +638,9 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     asm volatile("" : "+s"(map.use_index), "+s"(map.use_cells), "+s"(map.n_edge), "+s"(map.n_poly));
     SyncSlot<T>& xd = X.d[it & 1];
     SY_MARK(0);
+#ifndef SIT_ABL_NO_A
     __syncthreads();   // A: this step's positions
+#endif
     SY_MARK(1);
 #ifndef SIT_ABL_PO   // timing ablation: P0 writes no outputs
     if (TYPE == 0 && it >= 1) outputs(it - 1);

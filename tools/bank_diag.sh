@@ -16,9 +16,9 @@ run() {
   python3 tools/pmc_summary.py $out/$tag k_env_steps_sync 1 > $out/$tag.json
 }
 B="python3 bench.py --no-cpu-baseline --no-extra-lines --no-c5 --steps 20000 --warmup 40000"
-run lds rocprofv3 --kernel-trace --pmc $CNT -d $out/lds -o run --output-format csv -- $B
-SIT_LDS_MAP=0 run global rocprofv3 --kernel-trace --pmc $CNT -d $out/global -o run --output-format csv -- $B
-run nogather rocprofv3 --kernel-trace --pmc $CNT -d $out/nogather -o run --output-format csv -- $B --no-gather
+run lds rocprofv3 --kernel-trace --pmc $CNT -d $out/lds/p1 -o run --output-format csv -- $B
+SIT_LDS_MAP=0 run global rocprofv3 --kernel-trace --pmc $CNT -d $out/global/p1 -o run --output-format csv -- $B
+run nogather rocprofv3 --kernel-trace --pmc $CNT -d $out/nogather/p1 -o run --output-format csv -- $B --no-gather
 find $out -name "*.csv" -size +1M -delete
 python3 - $out <<'PY'
 import json, sys

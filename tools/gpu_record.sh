@@ -19,10 +19,10 @@ tools/gpu_steps.sh \
 rc=$?
 python3 tools/pmc_summary.py $O/pmc_c3 k_env_steps_sync 8 > $O/pmc_summary_c3.json
 python3 tools/make_profile_json.py $O/pmc_summary_c3.json $O/pmc_f32_rollout.json --steps-per-launch 40000 \
-  --n-env 32768 --mode rollout --round 4 --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh --no-c5 (5 passes)"
+  --n-env 32768 --mode rollout --round 5 --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh --no-c5 (5 passes)"
 python3 tools/pmc_summary.py $O/pmc_c5 "k_env_steps_sync<float, 2" 8 > $O/pmc_summary_c5.json
 python3 tools/make_profile_json.py $O/pmc_summary_c5.json $O/pmc_f32_policy.json --steps-per-launch 64 \
-  --n-env 32768 --mode policy --round 4 --kernel "k_env_steps_sync<float, kPolicy> (sit_sync.h), in-kernel serving" \
+  --n-env 32768 --mode policy --round 5 --kernel "k_env_steps_sync<float, kPolicy> (sit_sync.h), in-kernel serving" \
   --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh $C5 (5 passes; HIP-graph replays, 1 stream group)"
 python3 tools/pmc_summary.py $O/pmc_c5 k_policy_actor 8 > $O/pmc_summary_actor.json
 python3 tools/pmc_summary.py $O/pmc_c5 k_policy_admit 8 > $O/pmc_summary_admit.json
