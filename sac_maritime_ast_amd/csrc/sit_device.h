@@ -465,12 +465,17 @@ struct Route {
     tn[i * stride] = in_;
     te[i * stride] = ie;
     nw += 1;
+    // the new next target is known without reading the table back: the final waypoint (k == i) or
+    // the entry just written (k + 1 == i).  (load_next here put a global load round trip, ~1 500
+    // cycles, on the obstacle's critical segment at most sampling events.)
     if (k == i) {                         // the leg pointed at the final waypoint
       cn = in_; ce = ie;
       leg_geom(pn, pe, cn, ce, alpha, sa, ca);
-      load_next(k);
+      nn = end_n; ne = end_e;
+      leg_geom(cn, ce, nn, ne, alpha_n, sa_n, ca_n);
     } else if (k + 1 == i) {              // the next target was the final waypoint
-      load_next(k);
+      nn = in_; ne = ie;
+      leg_geom(cn, ce, nn, ne, alpha_n, sa_n, ca_n);
     }
     return true;
   }
