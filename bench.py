@@ -68,10 +68,9 @@ def parse():
     ap.add_argument("--groups", type=int, default=2, help="policy mode: env groups on separate streams")
     ap.add_argument("--request-div", type=int, default=4,
                     help="policy mode, --serve queue: request capacity = envs / this")
-    ap.add_argument("--serve", choices=("kernel", "queue", "concurrent"), default="kernel",
-                    help="policy mode: the step kernel serves its waiting envs itself at the launch's end "
-                         "(default), a server kernel beside the launch serves them within a few steps "
-                         "(concurrent; eager launches), or the request queue + sit_policy_actor between launches")
+    ap.add_argument("--serve", choices=("kernel", "queue"), default="kernel",
+                    help="policy mode: the step kernel serves its waiting envs itself (default), or the request "
+                         "queue + sit_policy_actor between launches")
     ap.add_argument("--graph-launches", type=int, default=16, help="policy mode: launches per HIP graph")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-baseline-workers", type=int, default=16,
@@ -86,8 +85,6 @@ def parse():
     ap.add_argument("--c5-warmup", type=int, default=32 * 16 * 60, help="warm-up steps of the C5 line")
     ap.add_argument("--c5-groups", type=int, default=1, help="C5 line: stream groups (1 measured fastest)")
     ap.add_argument("--c5-chunk", type=int, default=64, help="C5 line: env steps per launch")
-    ap.add_argument("--c5-serve", choices=("kernel", "queue", "concurrent"), default="kernel",
-                    help="C5 line: how waiting envs are served (see --serve)")
     ap.add_argument("--no-extra-lines", action="store_true",
                     help="rollout mode: skip the secondary lines (C3 in float64, C5 with the PyTorch-ROCm actor)")
     ap.add_argument("--trajectory-stride", type=int, default=0,
@@ -503,10 +500,7 @@ def bench_policy(args, rank, world, dev):
 
     n_env, G, chunk = args.n_env, args.groups, args.chunk
     per = n_env // G
-    # concurrent serving: eager launches (the server kernel runs on a stream of the handle's beside each
-    # launch; long chunks cost no idle envs, so the per-launch host work is amortised without a graph)
-    eager = args.serve == "concurrent"
-    per_graph = 1 if eager else max(1, min(args.graph_launches, max(1, args.steps // chunk)))
+    per_graph = max(1, min(args.graph_launches, max(1, args.steps // chunk)))
     gathering = not args.no_gather
     # transitions of one graph replay per group: 1 per ~390 env-steps measured (C3), 1 per 96 here
     tcap = per * chunk * per_graph // 96 if gathering else 0
@@ -519,7 +513,7 @@ def bench_policy(args, rank, world, dev):
                                 precision=args.precision, device=dev)
         env.reset()
         env.init_step()
-        cap = None if args.serve in ("kernel", "concurrent") else max(256, per // args.request_div)
+        cap = None if args.serve == "kernel" else max(256, per // args.request_div)
         samplers.append(PolicySampler(env, policy, chunk=chunk, seed=args.seed, env_id_offset=off,
                                       request_capacity=cap, transition_capacity=tcap, serve=args.serve,
                                       fused_actor=not getattr(args, "torch_actor", False)))
@@ -538,19 +532,15 @@ def bench_policy(args, rank, world, dev):
     torch.cuda.synchronize(dev)
     launch_ms = [a.elapsed_time(b) for row in ev for a, b in row]
     kern = kernel_name(samplers[0].env)
-    # the timed loop: HIP-graph replays of `per_graph` launches of every group (concurrent: eager launches)
-    if not eager:
-        (runner or samplers[0]).capture(per_graph)
+    # the timed loop: HIP-graph replays of `per_graph` launches of every group
+    (runner or samplers[0]).capture(per_graph)
     n_rep = max(2, args.steps // (chunk * per_graph))
     n_warm = max(1, args.warmup // (chunk * per_graph))
     gathers = [AsyncTransitionGather(tcap, 24, samplers[0].env.dtype, dev, world) for _ in range(G)] if gathering else []
     rep_no = [0]
 
     def replay():
-        if eager:
-            (runner or samplers[0]).launch()
-        else:
-            (runner or samplers[0]).replay()
+        (runner or samplers[0]).replay()
         i = rep_no[0]
         for g, (sm, ga) in enumerate(zip(samplers, gathers)):
             rec, cnt = ga.buffers(i)
@@ -591,12 +581,11 @@ def bench_policy(args, rank, world, dev):
                        "evaluated in HIP for the envs waiting at each sampling event) and the HIP env step"
                        if world == 1 else
                        f"C5 x{world}: {2 * n_env * world} policy-driven ships sharded over {world} GPUs",
-           "actor": ({"kernel": "in the step kernel (sit_rollout_args.actor_weights), at the launch's end",
-                      "concurrent": "k_actor_server beside each launch (sit_rollout_args.actor_concurrent)",
-                      }.get(args.serve, "sit_policy_actor (fused) on the request queue, capacity n/" + str(args.request_div)))
+           "actor": ("in the step kernel (sit_rollout_args.actor_weights)" if args.serve == "kernel" else
+                     "sit_policy_actor (fused) on the request queue, capacity n/" + str(args.request_div))
                     if all(sm.fused for sm in samplers) else "PyTorch-ROCm",
            "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env, "fused_steps_per_launch": chunk,
-           "mode": "policy", "stream_groups": G, "launches_per_hip_graph": 0 if eager else per_graph,
+           "mode": "policy", "stream_groups": G, "launches_per_hip_graph": per_graph,
            "parallelism": f"env-shard x{world}",
            "env_step_fraction": env_steps / (world * n_env * n_launch * chunk),
            "policy_evaluations": int(sum(int(sm.served.item()) for sm in samplers))}
@@ -629,7 +618,7 @@ def main():
     if args.mode == "rollout" and not args.no_c5:
         # config C5 beside the headline C3/C4 line: policy mode, driver-timed in the same run
         a5 = argparse.Namespace(**vars(args))
-        a5.mode, a5.chunk, a5.groups, a5.serve = "policy", args.c5_chunk, args.c5_groups, args.c5_serve
+        a5.mode, a5.chunk, a5.groups = "policy", args.c5_chunk, args.c5_groups
         a5.steps, a5.warmup = max(args.c5_steps, a5.chunk * 16 * 2), args.c5_warmup
         c5 = bench_policy(a5, rank, world, dev)
     extra = {}

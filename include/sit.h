@@ -400,33 +400,10 @@ typedef struct sit_rollout_args {
   const float* actor_weights;  /* float32[SIT_ACTOR_WEIGHTS] (sit_policy_actor's layout) or NULL */
   int32_t actor_deterministic; /* nonzero: x = mu (no sampling noise) */
   int64_t* actor_served;       /* int64[1] or NULL: += envs served */
-  /* Concurrent serving (with actor_weights, optional).  With actor_concurrent != 0 the actor is not
-   * evaluated at the end of the launch but by a second kernel that runs beside it (on a stream of the
-   * handle's, forked from `stream` after zeroing the launch's control block and joined back into it):
-   * an env that stops at a sampling event publishes a request — the observation it waits at, the
-   * event's tag — and steps again as soon as its action slot carries the answer, usually a few steps
-   * later in the same launch.  The actions are those of the in-kernel path bit for bit (same network,
-   * same head, same normal draw, keyed by the event), so every env's sequence of executed steps equals
-   * the in-kernel path's; only how many SIT_ST_NO_STEP rows it writes, and where, depends on timing.
-   *   actor_slot  uint64[n_env]: {tag = the env's event counter + 1, float32 action bits}, zero-initialised
-   *               by the caller before the first launch and kept across launches; the readiness of an env
-   *               in this mode is its slot's tag (policy_ready is written for information only)
-   *   actor_req   uint64[SIT_OBS_DIM + 1][n_env]: request granules (the observation, then the event's
-   *               normal draw), zero-initialised, kept across launches
-   * The first concurrent launch of a handle allocates (not inside a stream capture); logged launches are
-   * refused.  sit_server_stats reports the server's passes and whether it ever gave up (its time bound,
-   * SIT_SRV_TIMEOUT_MS, default 2 s: an env whose request outlives a launch asks again at the next). */
-  uint64_t* actor_slot;
-  uint64_t* actor_req;
-  int32_t actor_concurrent;
 } sit_rollout_args;
 #define SIT_POLICY_READY 1    /* policy_ready: an action waits in policy_action[e] */
 #define SIT_POLICY_WAITING 2  /* policy_ready: the env stopped at a sampling event for its action */
 int sit_rollout(sit_handle* h, const sit_rollout_args* a, void* stream);
-/* Concurrent serving counters since the handle's first concurrent launch (or the last reset):
- * out[0] server blocks that left at their time bound, out[1] actor passes, out[2] rows served,
- * out[3] polls.  Synchronises the device. */
-int sit_server_stats(sit_handle* h, uint64_t* out, int32_t reset);
 size_t sit_rollout_args_size(void);
 /* Policy mode helper: the squashed Gaussian head of the actor (ast_core/distributions/normal.py:
  * 88-101, ast_core/policies/gaussian_policy.py:71-72) applied to the actor network's output and

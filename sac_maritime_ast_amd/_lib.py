@@ -86,7 +86,6 @@ class RolloutArgs(ctypes.Structure):
         ("request_capacity", c_int32),
         ("env_steps", c_void_p), ("log", c_void_p), ("request_age", c_void_p),
         ("actor_weights", c_void_p), ("actor_deterministic", c_int32), ("actor_served", c_void_p),
-        ("actor_slot", c_void_p), ("actor_req", c_void_p), ("actor_concurrent", c_int32),
     ]
 
 
@@ -109,7 +108,6 @@ SIGNATURES = {
     "sit_debug_flags": (c_int32, [c_void_p]),
     "sit_debug_build": (c_int32, []),
     "sit_role_fallbacks": (c_int32, [c_void_p, c_int32]),
-    "sit_server_stats": (c_int32, [c_void_p, c_void_p, c_int32]),
     "sit_load_map": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "sit_load_routes": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "sit_load_initial": (c_int32, [c_void_p, c_void_p]),

@@ -160,13 +160,6 @@ struct StepIO {
   int32_t actor_det;
   unsigned long long* actor_served;
   T* log;                 // [n_steps][SIT_LOG_ROWS][n_env] or null
-  // concurrent serving (sit_serve.h, k_actor_server beside the launch): the action granules [n_env]
-  // (or null), the request granules [SIT_OBS_DIM][n_env], and the launch's control block (the handle's)
-  unsigned long long* srv_slot;
-  unsigned long long* srv_req;
-  const float* srv_w;             // the server's packed actor weights
-  unsigned long long* srv_mask;   // [step blocks]
-  unsigned* srv_done;             // finished step blocks
 };
 
 template <typename T>
@@ -1294,14 +1287,6 @@ struct sit_handle {
   bool have_map = false, have_routes = false, have_init = false;
   unsigned char* stage = nullptr;       // sit_step_host: pinned coherent host staging
   unsigned char* stage_dev = nullptr;   // its device address
-  // concurrent serving (k_actor_server, sit_serve.h): the handle's second stream and its fork / join
-  // events, the launch's control block (mask per step block, finished count; zeroed per launch) and
-  // the server's counters (timeouts, passes, rows, polls; kept across launches)
-  hipStream_t srv_stream = nullptr;
-  hipEvent_t srv_fork = nullptr, srv_join = nullptr;
-  unsigned char* srv_ctl = nullptr;
-  size_t srv_ctl_bytes = 0;
-  unsigned long long* srv_stats = nullptr;
 };
 
 namespace {
@@ -1600,44 +1585,6 @@ size_t sync_launch_lds(const sit_handle* h, const StepIO<T>& io, bool* lds_map, 
   return lds + SIT_DYN_OFF;
 }
 
-// concurrent serving: server blocks (SIT_SRV_BLOCKS, at least one per kSrvAssign step blocks) and
-// the server's time bound (SIT_SRV_TIMEOUT_MS, default 2 000 ms; s_memrealtime runs at 100 MHz)
-inline int srv_blocks(int blocks) {
-  static const int env_n = [] { const char* e = std::getenv("SIT_SRV_BLOCKS"); return e ? std::atoi(e) : 0; }();
-  const int want = env_n > 0 ? env_n : SIT_SRV_BLOCKS;
-  return std::max(std::min(want, blocks), (blocks + kSrvAssign - 1) / kSrvAssign);
-}
-inline uint64_t srv_timeout_ticks() {
-  static const uint64_t ms = [] { const char* e = std::getenv("SIT_SRV_TIMEOUT_MS"); return e ? (uint64_t)std::atoll(e) : 2000ull; }();
-  return ms * 100000ull;
-}
-// the control block (allocated by the first concurrent launch, which must not be captured), zeroed on
-// `stream`, and the server stream made to follow it
-inline int srv_prepare(sit_handle* h, int blocks, hipStream_t stream) {
-  const size_t bytes = ((size_t)blocks * 8 + 4 + 15) & ~size_t(15);
-  if (!h->srv_stream || h->srv_ctl_bytes < bytes) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    HIP_TRY(h, hipStreamIsCapturing(stream, &cs));
-    if (cs != hipStreamCaptureStatusNone)
-      return fail(h, SIT_E_STATE, "the first concurrent-serving launch of a handle allocates: run it before capturing");
-    if (!h->srv_stream) {
-      HIP_TRY(h, hipStreamCreateWithFlags(&h->srv_stream, hipStreamNonBlocking));
-      HIP_TRY(h, hipEventCreateWithFlags(&h->srv_fork, hipEventDisableTiming));
-      HIP_TRY(h, hipEventCreateWithFlags(&h->srv_join, hipEventDisableTiming));
-      HIP_TRY(h, hipMalloc(reinterpret_cast<void**>(&h->srv_stats), 4 * sizeof(unsigned long long)));
-      HIP_TRY(h, hipMemset(h->srv_stats, 0, 4 * sizeof(unsigned long long)));
-    }
-    if (h->srv_ctl) HIP_TRY(h, hipFree(h->srv_ctl));
-    h->srv_ctl = nullptr;
-    HIP_TRY(h, hipMalloc(reinterpret_cast<void**>(&h->srv_ctl), bytes));
-    h->srv_ctl_bytes = bytes;
-  }
-  HIP_TRY(h, hipMemsetAsync(h->srv_ctl, 0, bytes, stream));
-  HIP_TRY(h, hipEventRecord(h->srv_fork, stream));
-  HIP_TRY(h, hipStreamWaitEvent(h->srv_stream, h->srv_fork, 0));
-  return SIT_OK;
-}
-
 template <typename T>
 int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
   KArgs<T> a = make_args<T>(h);
@@ -1679,45 +1626,12 @@ int launch_steps(sit_handle* h, const StepIO<T>& io, hipStream_t stream) {
     const int blocks = (h->n_env + kSyncLanes - 1) / kSyncLanes;
     a.lds_bytes = (int32_t)(lds_sync - SIT_DYN_OFF);
     a.fake_simds = h->fake_simds;
-    const bool srv = io.srv_slot != nullptr;
-    if (srv) {   // concurrent serving: the control block zeroed, the server stream forked off `stream`
-      if (mode != kPolicy || !io.srv_w || !io.srv_req || io.actor_w)
-        return fail(h, SIT_E_INVALID, "concurrent serving: policy mode with actor weights and request granules");
-      const int rc = srv_prepare(h, blocks, stream);
-      if (rc) return rc;
-      a.io.srv_mask = reinterpret_cast<unsigned long long*>(h->srv_ctl);
-      a.io.srv_done = reinterpret_cast<unsigned*>(h->srv_ctl + (size_t)blocks * 8);
-    }
     void* args[] = {&a};
     HIP_TRY(h, hipLaunchKernel(kern, dim3(blocks), dim3(256), args, lds_sync, stream));
     set_kernel_name<T>(h, true, mode, sync_lds, false, mach);
-    if (srv) {   // the server right behind it (it never holds the step kernel up: see sit_serve.h)
-      SrvArgs<T> sa{};
-      sa.w = io.srv_w;
-      sa.initial_state = a.sc.initial_state;
-      sa.slot = io.srv_slot;
-      sa.req = io.srv_req;
-      sa.mask = a.io.srv_mask;
-      sa.done = a.io.srv_done;
-      sa.stats = h->srv_stats;
-      sa.served = io.actor_served;
-      sa.seed = io.seed;
-      sa.env_id_offset = io.env_id_offset;
-      sa.timeout = srv_timeout_ticks();
-      sa.n_env = h->n_env;
-      sa.n_blocks = blocks;
-      sa.n_srv = srv_blocks(blocks);
-      sa.det = io.actor_det;
-      void* sargs[] = {&sa};
-      HIP_TRY(h, hipLaunchKernel(reinterpret_cast<const void*>(&k_actor_server<T>), dim3(sa.n_srv), dim3(256), sargs,
-                                 kSrvLds, h->srv_stream));
-      HIP_TRY(h, hipEventRecord(h->srv_join, h->srv_stream));
-      HIP_TRY(h, hipStreamWaitEvent(stream, h->srv_join, 0));
-    }
     return SIT_OK;
   }
   if (io.actor_w) return fail(h, SIT_E_INVALID, "in-kernel serving runs on k_env_steps_sync only");
-  if (io.srv_slot) return fail(h, SIT_E_INVALID, "concurrent serving runs on k_env_steps_sync only");
   const int blocks = (h->n_env + kEnvsPerBlock * kGroups - 1) / (kEnvsPerBlock * kGroups);
   // the map (edges, index, classes) is staged in LDS when it fits the budget next to the static
   // exchange buffers and the launch has enough steps to amortise the staging; otherwise the

@@ -155,17 +155,6 @@ int sit_role_fallbacks(uint64_t* count, int32_t reset) {
   *count = v;
   return rc;
 }
-int sit_server_stats(sit_handle* h, uint64_t* out, int32_t reset) {
-  if (!h || !out) return fail(h, SIT_E_INVALID, "need a handle and uint64[4]");
-  for (int i = 0; i < 4; ++i) out[i] = 0;
-#ifndef SIT_HOST_MEMORY_TEST
-  if (!h->srv_stats) return SIT_OK;
-  HIP_TRY(h, hipDeviceSynchronize());
-  HIP_TRY(h, hipMemcpy(out, h->srv_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  if (reset) HIP_TRY(h, hipMemset(h->srv_stats, 0, 4 * sizeof(uint64_t)));
-#endif
-  return SIT_OK;
-}
 size_t sit_rollout_args_size(void) { return sizeof(sit_rollout_args); }
 size_t sit_params_size(void) { return sizeof(sit_params); }
 
@@ -316,14 +305,6 @@ void sit_destroy(sit_handle* h) {
   if (h->map) (void)setup_free(h->map);
 #ifndef SIT_HOST_MEMORY_TEST
   if (h->stage) (void)hipHostFree(h->stage);
-  if (h->srv_stream) {   // (the server of the last launch has finished: the caller's stream joined it)
-    (void)hipStreamSynchronize(h->srv_stream);
-    (void)hipStreamDestroy(h->srv_stream);
-    (void)hipEventDestroy(h->srv_fork);
-    (void)hipEventDestroy(h->srv_join);
-  }
-  if (h->srv_ctl) (void)hipFree(h->srv_ctl);
-  if (h->srv_stats) (void)hipFree(h->srv_stats);
 #endif
   delete h;
 }
@@ -843,10 +824,7 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
   if (ra->policy_action && ra->action_ne)
     return fail(h, SIT_E_INVALID, "policy mode and explicit actions are exclusive");
   const bool serve = ra->policy_action && ra->actor_weights;
-  const bool conc = serve && ra->actor_concurrent;
   if (ra->actor_weights && !ra->policy_action) return fail(h, SIT_E_INVALID, "actor_weights need policy mode");
-  if (ra->actor_concurrent && (!serve || !ra->actor_slot || !ra->actor_req))
-    return fail(h, SIT_E_INVALID, "concurrent serving needs policy mode, actor_weights, actor_slot and actor_req");
   if (serve && !ra->policy_ready) return fail(h, SIT_E_INVALID, "policy mode needs policy_ready");
   if (ra->policy_action && !serve &&
       (!ra->policy_ready || !ra->request_env || !ra->request_noise || !ra->request_obs || !ra->request_count ||
@@ -872,12 +850,6 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
     io->actor_w = serve ? ra->actor_weights : nullptr;
     io->actor_det = ra->actor_deterministic;
     io->actor_served = reinterpret_cast<unsigned long long*>(ra->actor_served);
-    if (conc) {   // the step kernel publishes requests; k_actor_server answers them beside it
-      io->actor_w = nullptr;
-      io->srv_w = ra->actor_weights;
-      io->srv_slot = reinterpret_cast<unsigned long long*>(ra->actor_slot);
-      io->srv_req = reinterpret_cast<unsigned long long*>(ra->actor_req);
-    }
   };
   // policy mode: the step kernel, then the deterministic admission of the waiting envs into the
   // request queue (k_policy_admit, sit_actor.h) on the same stream — or, serving in the kernel, nothing;
@@ -885,11 +857,6 @@ int sit_rollout(sit_handle* h, const sit_rollout_args* ra, void* stream) {
   auto run = [&](auto* io, auto launch) -> int {
     using R = std::remove_pointer_t<decltype(io->next_state)>;
     sit_rollout_args q = *ra;
-    if (conc) {
-      if (sync_launch_lds<R>(h, *io, nullptr, nullptr) == 0)
-        return fail(h, SIT_E_INVALID, "concurrent serving needs the fused step kernel (no trajectory log)");
-      return launch(*io);
-    }
     if (serve && sync_launch_lds<R>(h, *io, nullptr, nullptr) == 0) {
       const ServeQueue sq = serve_queue(h);
       io->actor_w = nullptr;

@@ -85,9 +85,8 @@ constexpr uint32_t kPbTerrain = 1u << 0, kPbIw = 1u << 1, kPbArrive = 1u << 2, k
                    kPbColl = 1u << 4;   // kPbColl: the ship-ship collision, in the test ship's word (P0)
 // the episode ends: test ship arrival / horizon / terrain; obstacle horizon / terrain / IW; collision
 constexpr uint32_t kPbDoneTest = kPbArrive | kPbHorizon | kPbTerrain | kPbColl, kPbDoneObs = kPbHorizon | kPbTerrain | kPbIw;
-// the step's policy-mode decision (SyncSlot::q): the env steps / it waits for its action (at its
-// episode's first step: kQStalledInit)
-constexpr int32_t kQLive = -1, kQStalled = -2, kQStalledInit = -3;
+// the step's policy-mode decision (SyncSlot::q): the env steps / it waits for its action
+constexpr int32_t kQLive = -1, kQStalled = -2;
 
 template <typename T>
 struct SyncSlot {             // one step of the envs of a group (ring of 2)
@@ -161,10 +160,6 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   bool ready = false, stalled = false;
   T pa = T(0);
   int32_t age0 = 0;              // policy mode (D1): admission rounds waited (publish_ages)
-  // concurrent serving (policy mode with a.io.srv_slot, sit_serve.h): the last poll of the action
-  // slot (P1 publishes the request)
-  const bool srv = MODE == kPolicy && a.io.srv_slot != nullptr;
-  unsigned long long pv = 0;
   // D1: the next sampling event's action and IW direction, drawn ahead (after the dynamics of the
   // step that consumed the previous one, or in the prologue) so that the event itself, on the
   // critical segment before barrier A, costs two multiply-adds
@@ -206,11 +201,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       ab_len = a.sc.ab_len[env];
       ab_alpha = a.sc.ab_alpha[env];
       samp_limit = ieee_mul(ab_len, cs.x.theta);   // MSRL_env_ex.py:569
-      if (MODE == kPolicy && srv) {      // the action slot answers the request of this event
-        pv = srv_ld(&a.io.srv_slot[env]);
-        ready = (uint32_t)(pv >> 32) == event + 1u;
-        pa = (T)__uint_as_float((uint32_t)pv);
-      } else if (MODE == kPolicy) {
+      if (MODE == kPolicy) {
         ready = a.io.policy_ready[env] == SIT_POLICY_READY;
         pa = a.io.policy_action[env];
         age0 = a.io.request_age ? a.io.request_age[env] : 0;   // (NULL when the launch serves in-kernel)
@@ -225,7 +216,6 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     iw_dir(ab_alpha, nx_act * (M_PI / 6.0), nx_cs, nx_sn);
   };
   if (TYPE == 1 && act && (MODE == kSynth || (MODE == kPolicy && ready))) draw_next();
-
   if (MODE == kExplicit && TYPE == 1 && act && n > 0) load_inputs(0);
   T p0[6] = {}, p0lo[3] = {};
   int nw0 = 0;
@@ -280,7 +270,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
           // kernel after the launch queues its request, k_policy_admit)
           stalled = true;
           sac = false;
-          q = ep_step == 0 ? kQStalledInit : kQStalled;   // (concurrent serving: P1's request says which)
+          q = kQStalled;
         } else if (sac) {                 // the action drawn ahead (draw_next)
           act_n = nx_act;
           if (MODE == kPolicy) ready = false;
@@ -301,8 +291,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     __syncthreads();   // A: positions (and the IW, and in policy mode the step's decision) published
 #endif
     SY_MARK(1);
-    // (re-read every step: under concurrent serving an env steps again within the launch)
-    if (MODE == kPolicy && TYPE == 0 && act) stalled = xd.q[lane] != kQLive;
+    if (MODE == kPolicy && TYPE == 0 && act && !stalled) stalled = xd.q[lane] != kQLive;
     if (act && !stalled) {
       T o_rpm, o_ect, o_pme = T(0);
       bool ect_over = false;
@@ -430,18 +419,6 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         xsincos(s.psi, &sp_n, &cp_n);
       }
     }
-    if (srv && TYPE == 1) {   // concurrent serving: the waiting lanes poll their action slots
-      if (act && stalled) {
-        if ((uint32_t)(pv >> 32) == event + 1u) {   // served: the env steps again from the next step
-          stalled = false;
-          ready = true;
-          pa = (T)__uint_as_float((uint32_t)pv);
-          draw_next();
-        } else {
-          pv = srv_ld(&a.io.srv_slot[env]);
-        }
-      }
-    }
     SY_MARK(4);
     SY_STEP();
 #ifdef SIT_PRIO_D1_B
@@ -469,11 +446,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
     }
   }
   static_assert(kSyncLanes == kAdmitGroup || MODE != kPolicy, "one wave = one admission group");
-  if (srv && TYPE == 1) {
-    // this block in the finished count (after barrier C, so after P1's last mask bits: the server
-    // leaves once every block is counted and it holds no request)
-    if (lane == 0) __hip_atomic_fetch_add((srv_gu32*)a.io.srv_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (MODE == kPolicy && TYPE == 1) {
+  if (MODE == kPolicy && TYPE == 1) {
     if (pub) {   // in-kernel serving: the waiting envs' ids and their events' normal draws, in lane order
       const bool w = act && stalled;
       const unsigned long long m = __ballot(w);
@@ -510,11 +483,6 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
   // it cost C3 1.4 %, a load, a store and three more SGPR spills.)
   T iw_tn = T(0), iw_te = T(0);
   bool iw_valid = false, iw_in = false;
-  // concurrent serving (P1, sit_serve.h): the obstacle's event counter (D1's, mirrored: +1 at every
-  // consumed event) and the lane's request (1: its granules stored this step, 2: one step ago)
-  const bool srv = MODE == kPolicy && TYPE == 1 && a.io.srv_slot != nullptr;
-  uint32_t p_event = (srv && act) ? a.st.event[env] : 0u;
-  uint32_t pub_age = 0;
   if (!LDSMAP && TYPE == 1 && act) {
     const uint32_t f = a.st.iwk_flags[env];
     iw_tn = a.st.iwk[0][env]; iw_te = a.st.iwk[1][env];
@@ -678,41 +646,7 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     if (TYPE == 0 && it >= 1) outputs(it - 1);
 #endif
     SY_MARK(7);
-    if (srv) {
-      // announce the requests stored one step ago: after this wave's vmcnt(0) their granules have
-      // landed, before the mask bit (MI355X_MICROARCH.md § visibility, R1)
-      const unsigned long long m = __ballot(pub_age == 2u);
-      if (m) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_fetch_or((srv_gu64*)&a.io.srv_mask[blockIdx.x], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      pub_age = pub_age == 1u ? 2u : 0u;
-      // an env that stops now asks: the observation it waits at (P0's: both ships after step it - 1,
-      // last_obs at the launch's first step, the initial observation at an episode start) and the
-      // event's normal draw, tag = event + 1
-      const int32_t qv = act ? xd.q[lane] : kQLive;
-      if (act && !stalled && qv != kQLive) {
-        unsigned long long* g = a.io.srv_req + env;
-        const size_t st = (size_t)n_env;
-        const uint32_t t32 = p_event + 1u;
-        const unsigned long long tag = (unsigned long long)t32 << 32;
-        const float nz = (float)(T)sampler_normal(a.io.seed, (uint64_t)(a.io.env_id_offset + env), p_event);
-        srv_st(g + SIT_OBS_DIM * st, tag | __float_as_uint(nz));
-        if (qv == kQStalledInit) {
-          srv_st(g, (unsigned long long)(t32 | kSrvInit) << 32);
-        } else if (it == 0) {
-          for (int q = 0; q < SIT_OBS_DIM; ++q)
-            srv_st(g + q * st, tag | __float_as_uint((float)a.st.last_obs[q * st + env]));
-        } else {
-          const SyncSlot<T>& xp = X.d[(it - 1) & 1];
-          for (int q = 0; q < 6; ++q) srv_st(g + q * st, tag | __float_as_uint((float)xp.t[q][lane]));
-          for (int q = 0; q < 4; ++q) srv_st(g + (6 + q) * st, tag | __float_as_uint((float)xp.o[q][lane]));
-        }
-        pub_age = 1;
-      }
-    }
-    if (MODE == kPolicy && act) stalled = xd.q[lane] != kQLive;
+    if (MODE == kPolicy && act && !stalled) stalled = xd.q[lane] != kQLive;
     // the predicates of the post-step position (MSRL_env_ex.py:460-603, 628-881): the map's (boundary
     // distance, hull in terrain, the IW test), arrival within 200 m of the final waypoint, the map
     // horizon, and (P0) the ship-ship collision.  (Reading the cell record and first edges before
@@ -755,7 +689,6 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
 #endif
     if (act && !stalled) {
       const uint32_t fl = xd.f[TYPE][lane];
-      if (srv && (fl & kSfSac)) ++p_event;   // D1 consumed an event's action
       int stop = (fl & kSfStopPre) ? 1 : 0;
       bool done = false;
       T r_nt = T(0), r_term = T(0);
@@ -823,13 +756,6 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
     SY_MARK(4);
     SY_STEP();
   }
-  if (srv) {   // the requests not announced yet, completed before barrier C (D1 then counts the block)
-    const unsigned long long m = __ballot(pub_age != 0u);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0 && m)
-      __hip_atomic_fetch_or((srv_gu64*)&a.io.srv_mask[blockIdx.x], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
   __syncthreads();   // C
   if (TYPE == 0) {
     if (n >= 1) outputs(n - 1);
@@ -867,8 +793,6 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
 #endif
 #if SIT_SYNC_WAVES_PER_EU > 0
 #define SIT_SYNC_OCC __attribute__((amdgpu_waves_per_eu(SIT_SYNC_WAVES_PER_EU, SIT_SYNC_WAVES_PER_EU)))
-#elif defined(SIT_SYNC_MAX_VGPRS)
-#define SIT_SYNC_OCC __attribute__((amdgpu_num_vgpr(SIT_SYNC_MAX_VGPRS)))
 #else
 #define SIT_SYNC_OCC
 #endif

@@ -252,27 +252,11 @@ class VecMultiShipRLEnv:
                           policy_io["actor_weights"].numel() != _lib.SIT_ACTOR_WEIGHTS):
                 raise ValueError("actor_weights: float32[SIT_ACTOR_WEIGHTS] (samplers.pack_actor_weights)")
             ra.actor_deterministic = int(bool(policy_io.get("actor_deterministic", False)))
-            if policy_io.get("actor_concurrent"):   # concurrent serving (k_actor_server beside the launch)
-                slot, greq = policy_io.get("actor_slot"), policy_io.get("actor_req")
-                if not serve or slot is None or greq is None:
-                    raise ValueError("concurrent serving needs actor_weights, actor_slot and actor_req")
-                if (slot.dtype != torch.int64 or slot.numel() != n or greq.dtype != torch.int64
-                        or greq.numel() != (_lib.SIT_OBS_DIM + 1) * n):
-                    raise ValueError("actor_slot: int64[n_env]; actor_req: int64[SIT_OBS_DIM + 1][n_env]")
-                ra.actor_slot, ra.actor_req, ra.actor_concurrent = slot.data_ptr(), greq.data_ptr(), 1
             req = policy_io.get("request_env")
             ra.request_capacity = 0 if req is None else int(req.numel())
         with torch.cuda.device(self.device):
             _lib.check(self.lib.sit_rollout(self.handle, byref(ra), self._stream()), self.handle)
         return out
-
-    def server_stats(self, reset: bool = False) -> dict:
-        """Concurrent serving counters (sit_server_stats): server blocks that left at their time bound,
-        actor passes, rows served, polls.  Synchronises the device."""
-        out = (ctypes.c_uint64 * 4)()
-        with torch.cuda.device(self.device):
-            self._call("sit_server_stats", ctypes.cast(out, c_void_p), int(bool(reset)))
-        return dict(zip(("timeouts", "passes", "rows", "polls"), (int(v) for v in out)))
 
     # ---------------- state ----------------
     def state_blob(self):

@@ -119,11 +119,7 @@ class PolicySampler:
 
     serve="kernel" (the default when the actor is fused and no request_capacity is given): the
     step kernel serves every env that ends a launch waiting, in the same launch (no queue, no
-    capacity).  serve="concurrent": a server kernel beside the launch answers each waiting env within
-    a few steps, so an env no longer waits for the launch's end (the same actions, bit for bit, so the
-    same per-env sequence of executed steps; which rows are ST_NO_STEP depends on timing) — long
-    chunks then cost nothing in idle envs.  serve="queue": the actor runs between launches on the
-    request queue;
+    capacity).  serve="queue": the actor runs between launches on the request queue;
     request_capacity bounds the envs served per launch (default n_env: every waiting env) and envs
     beyond it keep waiting, oldest first, for the next admission round.  The queued actor runs on a
     fixed number of rows (no host synchronisation); rows past the device-side request count are
@@ -147,9 +143,9 @@ class PolicySampler:
         self._w = pack_actor_weights(policy) if fused_actor and self.actor_dtype == torch.float32 else None
         if serve is None:
             serve = "kernel" if self._w is not None and request_capacity is None else "queue"
-        if serve not in ("kernel", "queue", "concurrent"):
-            raise ValueError("serve must be 'kernel', 'queue' or 'concurrent'")
-        if serve in ("kernel", "concurrent") and (self._w is None or request_capacity is not None):
+        if serve not in ("kernel", "queue"):
+            raise ValueError("serve must be 'kernel' or 'queue'")
+        if serve == "kernel" and (self._w is None or request_capacity is not None):
             raise ValueError("in-kernel serving needs the fused actor (the reference's architecture, float32) "
                              "and serves every waiting env (no request_capacity)")
         self.serve = serve
@@ -162,12 +158,8 @@ class PolicySampler:
         if self._w is not None:
             self._w = self._w.to(dev)
             self._w_version = self._weights_version()
-        if serve in ("kernel", "concurrent"):
+        if serve == "kernel":
             self.io.update(actor_weights=self._w, actor_served=self.served, actor_deterministic=bool(deterministic))
-            if serve == "concurrent":
-                self.io.update(actor_concurrent=True,
-                               actor_slot=torch.zeros(n, dtype=torch.int64, device=dev),
-                               actor_req=torch.zeros((_lib.SIT_OBS_DIM + 1, n), dtype=torch.int64, device=dev))
         else:
             cap = int(request_capacity or n)
             if cap <= 0:
@@ -211,7 +203,7 @@ class PolicySampler:
         events: optional (start, end) torch.cuda.Event pair recorded around the env kernel.
         first: the launch starts a new batch of replay transitions (their count is zeroed); later
         launches of a batch append to it, so a HIP graph of several launches keeps all of them."""
-        if (self.serve in ("kernel", "concurrent") and not torch.cuda.is_current_stream_capturing()
+        if (self.serve == "kernel" and not torch.cuda.is_current_stream_capturing()
                 and self._weights_version() != self._w_version):
             self.refresh_weights()
         if events is not None:
@@ -252,7 +244,7 @@ class PolicySampler:
         (sit_policy_apply), or for policies without a `.net` (mu, log_sigma) trunk forward() and a
         device-side scatter.  (Queue serving only: in-kernel serving has nothing left to do.)"""
         io, env = self.io, self.env
-        if self.serve in ("kernel", "concurrent"):
+        if self.serve == "kernel":
             return
         if self._w is not None:
             if not torch.cuda.is_current_stream_capturing() and self._weights_version() != self._w_version:

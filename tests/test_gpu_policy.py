@@ -828,58 +828,3 @@ def test_rollout_serving_argument_checks():
     assert "kPolicy" in env.lib.sit_step_kernel(env.handle).decode()
     # every env started at its episode's first sampling event with no action: served in the same launch
     assert (ready[:n] == _lib.SIT_POLICY_READY).all()
-
-
-# ------------------------------------------------------------------------------------------
-# concurrent serving (sit_rollout_args.actor_concurrent): k_actor_server beside the launch answers
-# each waiting env within a few steps (csrc/sit_serve.h)
-# ------------------------------------------------------------------------------------------
-_ROW_KEYS = ("next_state", "reward", "done", "status", "action")
-
-
-def _executed(launches, n):
-    """Per env, its executed rows (status without ST_NO_STEP), in order, over a list of launches."""
-    cat = {key: torch.cat([o[key] for o in launches]) for key in _ROW_KEYS}
-    live = ((cat["status"].to(torch.int64) & _lib.ST_NO_STEP) == 0).numpy()
-    return cat, live
-
-
-@pytest.mark.parametrize("precision", [32, 64])
-def test_concurrent_serving_equals_in_kernel(precision):
-    """Concurrent serving against in-kernel serving from the same start: the actions are the same bits
-    (same network, head and event-keyed draw), so every env executes the same sequence of steps — its
-    next_state / reward / done / status / action rows, ST_NO_STEP rows left out, are identical over the
-    common prefix — while the concurrent envs wait a few steps instead of until the launch's end
-    (more executed steps, env_step_fraction >= 0.9 after the first launch), and the server never
-    reaches its time bound."""
-    n, chunk, n_launch = (4000, 64, 8) if precision == 32 else (1000, 64, 6)   # (a partial last block)
-    _, (k, c) = _serving_samplers(n, precision, chunk, ("kernel", "concurrent"))
-    assert c.serve == "concurrent" and "actor_slot" in c.io
-    c.env.server_stats(reset=True)
-    outs_k, outs_c, steps_c = [], [], []
-    for it in range(n_launch):
-        before = int(c.env_steps.item())
-        ok, oc = k.launch(), c.launch()
-        torch.cuda.synchronize()
-        outs_k.append({key: ok[key].cpu().clone() for key in _ROW_KEYS})
-        outs_c.append({key: oc[key].cpu().clone() for key in _ROW_KEYS})
-        steps_c.append(int(c.env_steps.item()) - before)
-    st = c.env.server_stats()
-    assert st["timeouts"] == 0, st
-    assert st["rows"] > 0 and st["passes"] > 0, st
-    assert int(c.served.item()) == st["rows"]
-    assert int(c.env_steps.item()) > int(k.env_steps.item())
-    frac = np.array(steps_c[1:]) / (n * chunk)
-    assert frac.min() >= 0.9, frac
-    rk, lk = _executed(outs_k, n)
-    rc, lc = _executed(outs_c, n)
-    compared = 0
-    for e in range(n):
-        ik, ic = np.nonzero(lk[:, e])[0], np.nonzero(lc[:, e])[0]
-        m = min(len(ik), len(ic))
-        assert m >= chunk * (n_launch - 2), (e, len(ik), len(ic))
-        for key in _ROW_KEYS:
-            a, b = rk[key][ik[:m], e], rc[key][ic[:m], e]
-            assert _same(a.double(), b.double()) if a.is_floating_point() else torch.equal(a, b), (e, key)
-        compared += m
-    assert compared > n * chunk * (n_launch - 2)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Config C5 throughput of in-kernel vs concurrent serving, eager launches, one GPU:
+"""Config C5 throughput of in-kernel serving by chunk length, eager launches, one GPU (the concurrent
+server of commit 14a3fac took serve="concurrent"):
    python tools/conc_probe.py [--n-env 32768] [--chunks 64,256,1024] [--seconds 2]
 Prints env-steps/s, env_step_fraction and the server's counters per (serve, chunk)."""
 import argparse
@@ -17,7 +18,7 @@ from sac_maritime_ast_amd.samplers import GaussianPolicy, PolicySampler  # noqa:
 ap = argparse.ArgumentParser()
 ap.add_argument("--n-env", type=int, default=32768)
 ap.add_argument("--chunks", default="64,256,1024")
-ap.add_argument("--serves", default="kernel,concurrent")
+ap.add_argument("--serves", default="kernel")
 ap.add_argument("--seconds", type=float, default=2.0)
 ap.add_argument("--warm-steps", type=int, default=30720)
 args = ap.parse_args()
