@@ -576,8 +576,13 @@ class MultiShipRLEnv:
         a[1] = converted_action[1]
         self._sac[0] = 1 if SAC_update else 0
         self._init[0] = 1 if init else 0
-        with torch.cuda.device(self.vec.device):
+        dev = self.vec.device
+        # (the device context costs ~4 us per call: skipped when the handle's device is current)
+        if dev.index is None or torch.cuda.current_device() == dev.index:
             rc = self._step_fn(*self._step_args, self.vec._stream())
+        else:
+            with torch.cuda.device(dev):
+                rc = self._step_fn(*self._step_args, self.vec._stream())
         if rc:
             _lib.check(rc, self.vec.handle)
         # recording envs have the post-step state on the host; otherwise a view fetches it on demand

@@ -211,9 +211,18 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   // the next event's draw: mode-0 action U[-1, 1] (uniform_policy.py:20-22) from the sampler, or the
   // policy's squashed action in [-1, 1]; the route angle is the action scaled by pi / 6
   auto draw_next = [&]() {
+#if defined(SIT_ABL_CHEAPDRAW)   // timing ablation (results wrong): a hash draw instead of Philox
+    const uint32_t hh = (uint32_t)(env * 2654435761u) ^ (event * 0x9E3779B9u);
+    nx_act = MODE == kPolicy ? (double)pa : (double)(hh >> 8) * (2.0 / 16777216.0) - 1.0;
+#else
     nx_act = MODE == kPolicy ? (double)pa
                              : sampler_uniform(opaque_seed(a.io.seed), (uint64_t)(a.io.env_id_offset + env), event) * 2.0 - 1.0;
+#endif
+#if defined(SIT_ABL_NOTRIG)      // timing ablation (results wrong): no sincos of the IW direction
+    nx_cs = (T)(0.5 + 0.1 * nx_act); nx_sn = (T)(0.5 - 0.1 * nx_act);
+#else
     iw_dir(ab_alpha, nx_act * (M_PI / 6.0), nx_cs, nx_sn);
+#endif
   };
   if (TYPE == 1 && act && (MODE == kSynth || (MODE == kPolicy && ready))) draw_next();
   if (MODE == kExplicit && TYPE == 1 && act && n > 0) load_inputs(0);
