@@ -89,8 +89,14 @@ __device__ __forceinline__ float actor_head(float mu, float ls_raw, float noise,
 // ------------------------------------------------------------------------------------------
 // In-kernel serving
 // ------------------------------------------------------------------------------------------
-constexpr int kServeRows = 16;   // request rows per pass of the block's actor
-constexpr int kServeKB = 8;      // W2^T float4 rows per prefetch batch and lane (two batches in flight)
+#ifndef SIT_SERVE_ROWS
+#define SIT_SERVE_ROWS 16
+#endif
+constexpr int kServeRows = SIT_SERVE_ROWS;   // request rows per pass of the block's actor (even)
+#ifndef SIT_SERVE_KB
+#define SIT_SERVE_KB 8
+#endif
+constexpr int kServeKB = SIT_SERVE_KB;   // W2^T float4 rows per prefetch batch and lane (two batches in flight)
 
 // the block's waiting envs, written after barrier C: env id and the event's normal draw by the
 // obstacle's D wave, the observation the env waits at by P0; rows in lane order
@@ -103,8 +109,8 @@ struct ServePub {
 // the actor's working set, at LDS offset 0 over the staged map and the exchange slots (dead after
 // barrier D)
 struct ServeWork {
-  f32x2 h1[kServeRows / 2][kActorHidden];       // layer-1 activations, row pairs interleaved (16 KB)
-  float part[2][kServeRows][kActorHidden];      // layer-2 half sums (32 KB)
+  f32x2 h1[kServeRows / 2][kActorHidden];       // layer-1 activations, row pairs interleaved (1 KB per row)
+  float part[2][kServeRows][kActorHidden];      // layer-2 half sums (2 KB per row)
   float head[2 * kServeRows];                   // (mu, log_sigma) per row
 };
 static_assert(sizeof(f32x2) * (kServeRows / 2) * kActorHidden == sizeof(float) * kServeRows * kActorHidden,
@@ -220,8 +226,9 @@ __device__ __forceinline__ void serve_pass(const float* __restrict__ w, const Se
   __syncthreads();
   // layer 3: (row, output) pairs x 16 lanes, each lane 16 units, then a 16-lane reduction
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int half = 0; half < (2 * R + 15) / 16; ++half) {
     const int pr = (j >> 4) + 16 * half, c = j & 15;
+    if (2 * R % 16 != 0 && pr >= 2 * R) break;   // (uniform per 16-lane group)
     const int r = pr >> 1, o = pr & 1;
     const float* v = w + kActorW3 + o * H + c * 16;
     float sum = 0.0f;

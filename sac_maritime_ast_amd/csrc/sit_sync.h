@@ -59,8 +59,8 @@ constexpr int kSyncLanes = SIT_SYNC_LANES;
 // SIT_DIAG_SYNC (diagnostic builds only, tools/diag_sync.py): shader cycles per role and loop segment,
 // lane 0 of each wave, summed into g_sit_diag[role >> 1][(role & 1) * 16 + segment]: 0 work before
 // barrier A, 1 wait at A, 2 work A -> B, 3 wait at B, 4 work after B, 5 wave-steps; 6 and 7 P0's
-// outputs of the previous step up to the row stores / the rest (part of 2); 8-11 sub-segments
-// (tools/diag_sync.py names them per role)
+// outputs of the previous step up to the row stores / the rest (part of 2); 8-11 sub-segments; D1 also
+// 6 / 7 / 14 (tools/diag_sync.py names them per role)
 #ifdef SIT_DIAG_SYNC
 #define SY_INIT() unsigned long long sy_t = __builtin_amdgcn_s_memtime(), sy_acc[16] = {}
 #define SY_MARK(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -346,6 +346,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
           ppn = pre_n; ppe = pre_e; ppn_lo = pre_ln; ppe_lo = pre_le;
           s.ticks += 1;
         }
+        SY_MARK(6);
         // is_obs_ship_navigation_failure (MSRL_env_ex.py:566-576); arrival and the map horizon are
         // the P wave's (a function of the position)
         const bool nav = ect_over || comp_val(samp, samp_lo) > samp_limit;
@@ -354,7 +355,9 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
         xd.o[4][lane] = MODE == kExplicit ? angle_or_nan(false, T(0)) : (T)act_n;
         xd.f[1][lane] = fl;
         xd.ep[lane] = ep_step;
+        SY_MARK(7);
         if (MODE == kSynth && sac) draw_next();   // the next event's action (its counter is event)
+        SY_MARK(14);
       } else {
         // test_step (MSRL_Env.py:219-285)
         T rudder, thr, psi_ref;
@@ -684,6 +687,7 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
           iw_tn = wn; iw_te = we; iw_valid = true;
         }
         if (outside(c, wn, we, T(0)) || iw_in) pbits |= kPbIw;   // Q11
+        SY_MARK(11);
       } else {
         coll_t = closer_than(sn, se, xd.pn[1][lane], xd.pe[1][lane], c.coll_d2);   // MSRL_env_ex.py:584-603
         if (coll_t) pbits |= kPbColl;

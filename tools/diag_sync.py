@@ -23,16 +23,22 @@ import torch  # noqa: E402
 from sac_maritime_ast_amd import VecMultiShipRLEnv, _lib, make_scenario  # noqa: E402
 
 SEGS = ["work before A", "wait A", "work A->B", "wait B", "work after B"]
+# (The marks pin instruction order inside a basic block only: the compiler still moves work across
+# block boundaries — round 5 found the next heading's sincos and dynamics tail after D1's mark 9, so the
+# sub-segment D1 6 ("travelled distance") holds them too.  The five segments are exact.)
 # sub-segments (part of the segment named first): D 10 = sincos + Euler position (before A), 8 = guidance
 # and control, 9 = machinery and kinetics (A->B), 11 = the episode-end decision (after B, the rest is the
 # reset); P 8 = cell record + first edge group issued, 9 = boundary distance, 10 = hull test (A->B);
 # P0 6 / 7 = the previous step's outputs up to the row stores / after them (A->B)
 SUB = {"D": {10: ("work before A", "Euler position"), 8: ("work A->B", "dynamics base + guidance + control"),
              9: ("work A->B", "machinery + kinetics + next heading trig"),
+             6: ("work A->B", "D1: travelled distance (or the stop path)"),
+             7: ("work A->B", "D1: navigation test + publishing the step"),
+             14: ("work A->B", "D1: the next event's draw (synthetic sampler)"),
              11: ("work after B", "episode-end decision")},
        "P": {6: ("work A->B", "P0 outputs up to the row stores"), 7: ("work A->B", "P0 outputs after the stores"),
              8: ("work A->B", "cell record + first edges"), 9: ("work A->B", "boundary distance"),
-             10: ("work A->B", "hull test")}}
+             10: ("work A->B", "hull test"), 11: ("work A->B", "IW test (P1) / collision (P0)")}}
 ONCE = {12: "prologue (per launch)", 13: "epilogue (per launch)", 14: "barrier D + in-kernel serving (per launch)",
         15: "kernel start to the staged map (per launch)"}
 ROLES = ["D0 test dynamics", "D1 obstacle dynamics", "P0 test predicates+outputs", "P1 obstacle predicates"]
@@ -100,7 +106,8 @@ def main():
         launches = max(1, args.launches if not (args.policy or args.step) else 200)
         waves = launches * ((args.n_env + 63) // 64)
         for k, label in ONCE.items():   # per wave and launch
-            res[label] = round(row[k] / waves, 1)
+            if k not in sub or args.policy:
+                res[label] = round(row[k] / waves, 1)
         out["roles"][name] = res
     print(json.dumps(out, indent=1))
 
