@@ -37,19 +37,19 @@
 constexpr int kSyncLanes = SIT_SYNC_LANES;
 
 // Issue priority per role (s_setprio 0-3).  The two blocks on a CU put their waves on the SIMDs in
-// D/P pairs of different env groups, and the two waves of a SIMD compete for its issue slots where
-// both are ready.  The P waves carry the step's longest chains (P0: the previous step's outputs and
-// the test ship's map predicates before barrier B), the D waves have slack (D0 most): a total order
-// by that load — P0 > P1 > D1 > D0 — measured C3 +3.3 % and C5 +4.8 % (same-box A/B, two rounds;
-// favouring the D waves instead cost 1 - 2 %, giving both P waves the same level lost the gain on C3)
+// D/P pairs of different env groups — (D0, P0) and (D1, P1) — and the two waves of a SIMD compete for
+// its issue slots where both are ready.  Round 4, with P0 the longest chain: P0 > P1 > D1 > D0
+// measured C3 +3.3 % and C5 +4.8 % (same-box A/B, two rounds; favouring the D waves instead cost
+// 1 - 2 %).  Round 5: the double-float integrators made D1 the critical role, and D1 above
+// its partner P1 — P0 > D1 > P1 > D0 — measured C5 +0.7 %, C3 +0.1 % (three rounds, gpurun_out/r05s)
 #ifndef SIT_PRIO_P0
 #define SIT_PRIO_P0 3
 #endif
 #ifndef SIT_PRIO_P1
-#define SIT_PRIO_P1 2
+#define SIT_PRIO_P1 1
 #endif
 #ifndef SIT_PRIO_D1
-#define SIT_PRIO_D1 1
+#define SIT_PRIO_D1 2
 #endif
 #ifndef SIT_PRIO_D0
 #define SIT_PRIO_D0 0
