@@ -589,6 +589,16 @@ def bench_policy(args, rank, world, dev):
            "parallelism": f"env-shard x{world}",
            "env_step_fraction": env_steps / (world * n_env * n_launch * chunk),
            "policy_evaluations": int(sum(int(sm.served.item()) for sm in samplers))}
+    if samplers[0].fused:
+        # the cost of re-packing the fused actor's weights after an optimizer step (refresh_weights: the
+        # reference's SAC updates the policy between env steps, main_ast.py:350-362; here the natural
+        # granularity is a launch, so this is the price per policy update), host wall time with sync
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(20):
+            samplers[0].refresh_weights()
+        torch.cuda.synchronize(dev)
+        cfg["refresh_weights_us"] = (time.perf_counter() - t0) / 20 * 1e6
     if gathers:
         stats = torch.tensor([sum(ga.gathered for ga in gathers) - sum(x[0] for x in g0),
                               sum(ga.dropped() for ga in gathers) - sum(x[1] for x in g0)],
