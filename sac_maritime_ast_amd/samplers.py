@@ -106,11 +106,17 @@ def pack_actor_weights(policy: nn.Module, out: torch.Tensor | None = None) -> to
     if not shapes_ok:
         return None
     with torch.no_grad():
-        parts = [l1.weight.reshape(-1), l1.bias, l2.weight.t().reshape(-1), l2.bias, l3.weight.reshape(-1), l3.bias]
-        flat = torch.cat([t.detach().to(torch.float32).reshape(-1) for t in parts])
         if out is None:
-            return flat.contiguous()
-        out.copy_(flat)
+            parts = [l1.weight.reshape(-1), l1.bias, l2.weight.t().reshape(-1), l2.bias, l3.weight.reshape(-1), l3.bias]
+            return torch.cat([t.detach().to(torch.float32).reshape(-1) for t in parts]).contiguous()
+        # in place, one copy per parameter into its segment of the block (no concatenated temporary:
+        # half the host work of a refresh after each optimizer step)
+        o = 0
+        for t, shape in ((l1.weight, (H, _lib.SIT_OBS_DIM)), (l1.bias, (H,)), (l2.weight.t(), (H, H)), (l2.bias, (H,)),
+                         (l3.weight, (2, H)), (l3.bias, (2,))):
+            n = t.numel()
+            out[o:o + n].view(shape).copy_(t.detach())
+            o += n
         return out
 
 
