@@ -80,3 +80,28 @@ def test_oracle_policy_rollout_constant_policy_matches_explicit_actions():
     assert np.array_equal(r1["status"], r2["status"])
     ang = r1["action"][..., 2]
     assert np.allclose(ang[~np.isnan(ang)], 0.3 * np.pi / 6)
+
+
+def test_pack_actor_weights_in_place_equals_fresh_pack():
+    """The in-place refresh (one copy per parameter into its segment, PolicySampler.refresh_weights)
+    gives the same block as a fresh pack, before and after the parameters change (include/sit.h:
+    W1 [256][10], b1, W2 transposed [256 in][256 out], b2, W3 [2][256], b3)."""
+    from sac_maritime_ast_amd import _lib
+    from sac_maritime_ast_amd.samplers import pack_actor_weights
+    torch.manual_seed(3)
+    pol = GaussianPolicy(hidden=(256, 256))
+    fresh = pack_actor_weights(pol)
+    assert fresh.numel() == _lib.SIT_ACTOR_WEIGHTS and fresh.dtype == torch.float32
+    out = torch.full_like(fresh, float("nan"))
+    assert pack_actor_weights(pol, out=out) is out
+    assert torch.equal(out, fresh)
+    with torch.no_grad():
+        for p in pol.parameters():
+            p.add_(torch.randn_like(p))
+    pack_actor_weights(pol, out=out)
+    assert torch.equal(out, pack_actor_weights(pol))
+    l2 = pol.net[2]
+    H = _lib.SIT_ACTOR_HIDDEN
+    w2t = out[H * _lib.SIT_OBS_DIM + H:H * _lib.SIT_OBS_DIM + H + H * H].view(H, H)
+    assert torch.equal(w2t, l2.weight.detach().t())
+    assert pack_actor_weights(GaussianPolicy(hidden=(64, 64))) is None   # other architectures: generic path
