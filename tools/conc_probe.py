@@ -36,8 +36,6 @@ for serve in args.serves.split(","):
         for _ in range(max(2, args.warm_steps // chunk)):
             sm.launch(want)
         torch.cuda.synchronize()
-        if serve == "concurrent":
-            env.server_stats(reset=True)
         s0 = int(sm.env_steps.item())
         t0 = time.perf_counter()
         n_l = 0
@@ -54,8 +52,6 @@ for serve in args.serves.split(","):
         r = {"serve": serve, "chunk": chunk, "env_steps_per_s": steps / dt,
              "env_step_fraction": steps / (args.n_env * chunk * n_l), "launches": n_l,
              "ms_per_launch": 1e3 * dt / n_l}
-        if serve == "concurrent":
-            r["server"] = env.server_stats()
         print(json.dumps(r), flush=True)
         res.append(r)
         del sm, env
