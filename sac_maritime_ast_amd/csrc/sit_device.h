@@ -543,6 +543,18 @@ __device__ __forceinline__ T comp_fma(T hi, T& lo, T a, T b) {
     return hi + a * b;
   }
 }
+// per-integrator switches (experiments: which compensations the float32 drift needs)
+#ifndef SIT_COMP_PSI
+#define SIT_COMP_PSI 1   // the heading
+#endif
+#ifndef SIT_COMP_PI
+#define SIT_COMP_PI 1    // the heading PID and the ship-speed PI integrals
+#endif
+template <bool ON, typename T>
+__device__ __forceinline__ T comp_fma_if(T hi, T& lo, T a, T b) {
+  if constexpr (ON) return comp_fma(hi, lo, a, b);
+  else { (void)lo; return hi + a * b; }
+}
 template <typename T>
 __device__ __forceinline__ double comp_val(T hi, T lo) {
   if constexpr (kComp<T>) return ieee_add((double)hi, (double)lo);
@@ -655,13 +667,13 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
   // heading PID, error not wrapped (Q4)
   const T err = psi_ref - s.psi;
   const T derr = (err - s.hp) * c.inv_dt;
-  s.hi = comp_fma(s.hi, s.lhi, err, c.dt);
+  s.hi = comp_fma_if<SIT_COMP_PI != 0>(s.hi, s.lhi, err, c.dt);
   s.hp = err;
   const T out = err * c.kp_h + derr * c.kd_h + s.hi * c.ki_h;
   rudder = xclip(-out, -c.rudder_max, c.rudder_max);
   // cascaded PI, shaft PI measures the ship speed (Q2), no saturation (Q3)
   const T e1 = v_des - s.u;
-  s.i1 = comp_fma(s.i1, s.li1, e1, c.dt);
+  s.i1 = comp_fma_if<SIT_COMP_PI != 0>(s.i1, s.li1, e1, c.dt);
   const T wdes = e1 * c.kp1 + s.i1 * c.ki1;
   if (simpl_of<MACH>(c)) {
     // ThrottleFromSpeedSetPointSimplifiedPropulsion.throttle (controllers.py:170-172): the ship-speed
@@ -872,7 +884,7 @@ __device__ __forceinline__ void ship_dynamics_pos(const Consts<T>& c, Ship<T>& s
   s.e = e1;
   s.ln = ln1;
   s.le = le1;
-  s.psi = comp_fma(s.psi, s.lpsi, r, c.dt);
+  s.psi = comp_fma_if<SIT_COMP_PSI != 0>(s.psi, s.lpsi, r, c.dt);
   s.u = u + (c.inv_m11 * f0) * c.dt;
   s.v = v + (c.inv_m22 * f1) * c.dt;
   s.r = r + (c.inv_m33 * f2) * c.dt;
@@ -938,7 +950,7 @@ __device__ __forceinline__ void dyn_finish(const C& c, Ship<T>& s, const DynBase
   s.e = e1;
   s.ln = ln1;
   s.le = le1;
-  s.psi = comp_fma(s.psi, s.lpsi, r, c.dt);
+  s.psi = comp_fma_if<SIT_COMP_PSI != 0>(s.psi, s.lpsi, r, c.dt);
   s.u = u + (c.inv_m11 * b.f0) * c.dt;
   s.v = v + (c.inv_m22 * (b.f1 + f_rv)) * c.dt;
   s.r = r + (c.inv_m33 * (b.f2 + f_rr)) * c.dt;
