@@ -632,7 +632,9 @@ def main():
         a5.steps, a5.warmup = max(args.c5_steps, a5.chunk * 16 * 2), args.c5_warmup
         c5 = bench_policy(a5, rank, world, dev)
     extra = {}
-    if args.mode == "rollout" and not args.no_extra_lines and args.precision == 32:
+    # (single-GPU runs only: the scaling runs time the headline and the C5 line; the secondary lines
+    # would add two more sharded phases per N without adding a scaling measurement)
+    if args.mode == "rollout" and not args.no_extra_lines and args.precision == 32 and world == 1:
         # secondary lines (not the headline): C3 in the reference's own float64 arithmetic, and C5 with the
         # actor forward in PyTorch-ROCm on the request queue, two stream groups (north_star's C5 wording)
         a64 = argparse.Namespace(**vars(args))
