@@ -468,7 +468,7 @@ __device__ __forceinline__ void store4(double* p, double a, double b, double c, 
 __device__ __forceinline__ void iw_point(float n, float e, double ab_len, double ab_alpha, double ang, float& iwn,
                                          float& iwe) {
   float sn, cs;
-  sincosf((float)(ab_alpha + ang), &sn, &cs);
+  xsincos((float)(ab_alpha + ang), &sn, &cs);
   iwn = n + (float)ab_len * cs;
   iwe = e + (float)ab_len * sn;
 }
@@ -481,7 +481,7 @@ __device__ __forceinline__ void iw_point(double n, double e, double ab_len, doub
 // the same IW in two parts: the direction (cos, sin)(AB_alpha + a), which depends only on the action
 // (the sync kernel draws the next event's action ahead, off its critical segment), and the point
 __device__ __forceinline__ void iw_dir(double ab_alpha, double ang, float& cs, float& sn) {
-  sincosf((float)(ab_alpha + ang), &sn, &cs);
+  xsincos((float)(ab_alpha + ang), &sn, &cs);
 }
 __device__ __forceinline__ void iw_dir(double ab_alpha, double ang, double& cs, double& sn) {
   cs = cos(ab_alpha + ang);

@@ -1,8 +1,11 @@
 #!/bin/bash
-# drift (envs diverged, max) of each compensation variant
+# float32 drift (envs diverged, max) of library variants: tools/comp_drift.sh [lib ...]
+# (default: the round-5 compensation variants)
 set -u
 mkdir -p gpurun_out/compdrift
-for L in sac_maritime_ast_amd/libsit.so build_diag/libsit_nopsi.so build_diag/libsit_nopi.so build_diag/libsit_nopsipi.so; do
+LIBS=("$@")
+[ ${#LIBS[@]} -eq 0 ] && LIBS=(sac_maritime_ast_amd/libsit.so build_diag/libsit_nopsi.so build_diag/libsit_nopi.so build_diag/libsit_nopsipi.so)
+for L in "${LIBS[@]}"; do
   n=$(basename $L .so)
   SIT_LIBRARY=$L timeout -k 10 200 python tools/f32_drift.py --out gpurun_out/compdrift/$n.json > gpurun_out/compdrift/$n.log 2>&1 || { echo "$n failed"; exit 1; }
   python -c "
