@@ -189,7 +189,14 @@ constexpr int kMaxPolys = 32;
 #define SIT_FAST_TRIG 1
 #endif
 #if SIT_FAST_TRIG
-__device__ __forceinline__ void xsincos(float x, float* s, float* c) { *s = __sinf(x); *c = __cosf(x); }
+// v_sin / v_cos take the angle in revolutions and only |x / 2 pi| <= 256: the argument is scaled once
+// and reduced to [0, 1) with v_fract (exact), so any heading is valid; the scaling's float32 rounding
+// (~3e-8 relative of x) is below the float32 heading's own storage rounding at every magnitude
+__device__ __forceinline__ void xsincos(float x, float* s, float* c) {
+  const float rev = __builtin_amdgcn_fractf(x * 0.159154943091895336f);
+  *s = __builtin_amdgcn_sinf(rev);
+  *c = __builtin_amdgcn_cosf(rev);
+}
 #else
 __device__ __forceinline__ void xsincos(float x, float* s, float* c) { sincosf(x, s, c); }
 #endif
