@@ -183,8 +183,8 @@ constexpr int kMaxPolys = 32;
 // --------------------------------------------------------------------------------------
 // float32 sine / cosine (the heading's every step, the IW direction): the hardware's v_sin / v_cos
 // (argument scaled to revolutions; ~1e-6 absolute, within the float32 handle's 1e-5 contract) instead of
-// the library's range-reduced polynomial: C3 +2.6 %, C5 +0.9 % in a same-box A/B, float32 drift
-// unchanged (DESIGN.md §9).  0: sincosf.  The float64 handle keeps the library's sin / cos.
+// the library's range-reduced polynomial: C3 +2.9 %, C5 +1.6 % in same-box A/Bs, float32 drift
+// unchanged (DESIGN.md §4.5).  0: sincosf.  The float64 handle keeps the library's sin / cos.
 #ifndef SIT_FAST_TRIG
 #define SIT_FAST_TRIG 1
 #endif
