@@ -72,7 +72,8 @@ def parse():
                     help="policy mode: the step kernel serves its waiting envs itself (default), or the request "
                          "queue + sit_policy_actor between launches")
     ap.add_argument("--graph-launches", type=int, default=16, help="policy mode: launches per HIP graph")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=2.5,
+                    help="CPU work per baseline process (the whole leg takes ~2 s more for the imports)")
     ap.add_argument("--cpu-baseline-workers", type=int, default=16,
                     help="single-threaded oracle processes (the GPU box's CPU share is 16 cores per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -90,6 +91,8 @@ def parse():
     ap.add_argument("--trajectory-stride", type=int, default=0,
                     help="rollout mode: also gather every S-th step's trajectory rows (next_state, reward, done, "
                          "status) of every rank to rank 0 per launch (shard.TrajectoryGather; 0 = off)")
+    ap.add_argument("--actor-stream", action="store_true",
+                    help="policy mode, --serve queue: the actor on a HIP stream of its own (fork / join per launch)")
     ap.add_argument("--torch-actor", action="store_true",
                     help="policy mode: the actor forward in PyTorch-ROCm on the request queue (north_star's C5 "
                          "wording) instead of the fused HIP actor")
@@ -161,13 +164,21 @@ def cpu_baseline(seconds, seed, workers):
     """The oracle (float64 NumPy restatement, vectorised over envs) on a bounded sample of the same
     workload: per worker process 2048 envs (its own global env-id range), synthetic sampler,
     auto-reset, ~`seconds` of CPU work; `workers` single-threaded processes on the host cores
-    (one process per core).  Workers are fresh interpreters started as child
-    processes (nothing of this GPU process is forked into them); value = the env-steps all workers
+    (one process per core), one of them the scalar loop below, all at once (the leg
+    takes ~`seconds` + the imports).  Workers are fresh interpreters started as child processes
+    (nothing of this GPU process is forked into them); value = the env-steps all vectorised workers
     did / the slowest worker's time."""
     n_env = 2048
-    cores = max(1, min(workers, len(os.sched_getaffinity(0))))
+    share = max(1, min(workers, len(os.sched_getaffinity(0))))
+    cores = max(1, share - 1)
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1",
                PYTHONDONTWRITEBYTECODE="1")
+    # BASELINE.md CPU plan 2(a): the reference-equivalent scalar loop (one env, one process, one
+    # core), and through the calibration ratio measured in the build container
+    # (oracle/calibrate.py: reference / restatement at one env on one core) the reference's own
+    # estimated speed on this host, where the reference cannot run
+    sp = subprocess.Popen([sys.executable, "-c", CPU_WORKER, ROOT, "1", str(seconds), str(seed), "0"],
+                          stdout=subprocess.PIPE, env=env, text=True)
     procs = [subprocess.Popen([sys.executable, "-c", CPU_WORKER, ROOT, str(n_env), str(seconds), str(seed), str(p)],
                               stdout=subprocess.PIPE, env=env, text=True) for p in range(cores)]
     res = []
@@ -178,15 +189,10 @@ def cpu_baseline(seconds, seed, workers):
         res.append(json.loads(outp.strip().splitlines()[-1]))
     total = sum(r["env_steps"] for r in res)
     dt = max(r["seconds"] for r in res)
-    # BASELINE.md CPU plan 2(a): the reference-equivalent scalar loop (one env, one process, one
-    # core), and through the calibration ratio measured in the build container
-    # (oracle/calibrate.py: reference / restatement at one env on one core) the reference's own
-    # estimated speed on this host, where the reference cannot run
-    sp = subprocess.run([sys.executable, "-c", CPU_WORKER, ROOT, "1", str(max(2.0, seconds / 2)), str(seed), "0"],
-                        capture_output=True, env=env, text=True)
+    sp_out, _ = sp.communicate()
     scalar = None
     if sp.returncode == 0:
-        r1 = json.loads(sp.stdout.strip().splitlines()[-1])
+        r1 = json.loads(sp_out.strip().splitlines()[-1])
         scalar = {"value": r1["env_steps"] / r1["seconds"], "unit": "env-steps/s", "cores": 1,
                   "sample": f"oracle/sit_oracle.py with one env, {r1['steps']} steps, {r1['seconds']:.1f} s"}
         cal = latest_calibration()
@@ -516,7 +522,8 @@ def bench_policy(args, rank, world, dev):
         cap = None if args.serve == "kernel" else max(256, per // args.request_div)
         samplers.append(PolicySampler(env, policy, chunk=chunk, seed=args.seed, env_id_offset=off,
                                       request_capacity=cap, transition_capacity=tcap, serve=args.serve,
-                                      fused_actor=not getattr(args, "torch_actor", False)))
+                                      fused_actor=not getattr(args, "torch_actor", False),
+                                      actor_stream=getattr(args, "actor_stream", False) and args.serve == "queue"))
     runner = OverlappedPolicySampler(samplers) if G > 1 else None
     cur = torch.cuda.current_stream(dev)
     # kernel duration of the env launches: eager launches through the sampler (HIP events on each
@@ -586,6 +593,7 @@ def bench_policy(args, rank, world, dev):
                     if all(sm.fused for sm in samplers) else "PyTorch-ROCm",
            "envs_per_gpu": n_env, "ships_per_gpu": 2 * n_env, "fused_steps_per_launch": chunk,
            "mode": "policy", "stream_groups": G, "launches_per_hip_graph": per_graph,
+           "actor_on_own_stream": samplers[0].actor_stream is not None,
            "parallelism": f"env-shard x{world}",
            "env_step_fraction": env_steps / (world * n_env * n_launch * chunk),
            "policy_evaluations": int(sum(int(sm.served.item()) for sm in samplers))}
@@ -636,7 +644,8 @@ def main():
     # would add two more sharded phases per N without adding a scaling measurement)
     if args.mode == "rollout" and not args.no_extra_lines and args.precision == 32 and world == 1:
         # secondary lines (not the headline): C3 in the reference's own float64 arithmetic, and C5 with the
-        # actor forward in PyTorch-ROCm on the request queue, two stream groups (north_star's C5 wording)
+        # actor forward in PyTorch-ROCm on the request queue, on a HIP stream of its own (north_star's C5
+        # wording); one group of 64-step launches (tools/c5_torch_sweep.sh, profiles/r06_c5_torch_sweep.json)
         a64 = argparse.Namespace(**vars(args))
         a64.precision, a64.chunk, a64.steps, a64.warmup = 64, 10000, 30000, 40000
         r64 = bench_rollout(a64, rank, world, dev)
@@ -646,8 +655,8 @@ def main():
                            "roofline": r64["roofline"]}
         if not args.no_c5:
             at = argparse.Namespace(**vars(args))
-            at.mode, at.chunk, at.groups, at.serve, at.torch_actor = "policy", 32, 2, "queue", True
-            at.steps, at.warmup = 32 * 16 * 8, 32 * 16 * 30
+            at.mode, at.chunk, at.groups, at.serve, at.torch_actor, at.actor_stream = "policy", 64, 1, "queue", True, True
+            at.steps, at.warmup = 64 * 16 * 8, 64 * 16 * 15
             rt = bench_policy(at, rank, world, dev)
             extra["c5_torch_actor"] = {
                 "metric": "env-steps/sec, 65 536 policy-driven ships per GPU (config C5), PyTorch-ROCm actor",

@@ -267,7 +267,9 @@ int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint
  * 4 a*b + b*a (each correctly rounded per operation, as numpy's float64), 5 sin(a), 6 cos(a),
  * 7 atan2(a, b) (the device math library the float64 path uses), 8 the fused step kernel's wave
  * roles (sync_role_of) for the SIMD assignment a (base 4, digit v = SIMD of wave v) and CU ticket b,
- * packed as role of wave v in base-4 digit v.  fast_tu != 0 runs the copy compiled with the float32
+ * packed as role of wave v in base-4 digit v, 9 / 10 sin / cos of (float)a as the float32 step takes
+ * them (xsincos), 11 atan((float)a), 12 atan2((float)a, (float)b) in float32, each widened to
+ * float64.  fast_tu != 0 runs the copy compiled with the float32
  * step kernels' fast-math flags.  Device pointers. */
 int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, double* out, int32_t fast_tu,
                      void* stream);
@@ -410,10 +412,13 @@ size_t sit_rollout_args_size(void);
  * scattered into the env action slots, for request rows q < *request_count:
  *   x = mu + exp(clip(log_sigma, -20, 2)) * noise[q]   (x = mu when deterministic != 0)
  *   policy_action[request_env[q]] = tanh(x); policy_ready[request_env[q]] = 1
- * head real[capacity][head_stride] holds (mu, log_sigma) in its first two columns. */
+ * head real[capacity][head_stride] holds (mu, log_sigma) in its first two columns.
+ *   served   int64[1] or NULL: += min(*request_count, capacity) (the policy evaluations used, as
+ *            sit_policy_actor counts them) */
 int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t head_stride,
                      const void* noise, const int32_t* request_env, const int32_t* request_count,
-                     int32_t deterministic, void* policy_action, int32_t* policy_ready, void* stream);
+                     int32_t deterministic, void* policy_action, int32_t* policy_ready, int64_t* served,
+                     void* stream);
 /* Policy mode helper, the whole actor in one kernel: the SAC-AST Gaussian policy's MLP
  * (ast_core/nn_models/mlp.py:95-148: obs[SIT_OBS_DIM] -> 256 -> ReLU -> 256 -> ReLU -> (mu, log_sigma),
  * main_ast.py:67's hidden sizes) in float32 on request rows q < min(*request_count, capacity), then the

@@ -113,7 +113,7 @@ SIGNATURES = {
     "sit_load_initial": (c_int32, [c_void_p, c_void_p]),
     "sit_map_info": (c_int32, [c_void_p, c_void_p, c_int32]),
     "sit_policy_apply": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
-                                   c_void_p, c_void_p, c_void_p]),
+                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "sit_policy_actor": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sit_probe_map": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -42,7 +42,7 @@ import torch
 from . import _lib
 from .config import params as default_params
 from .config import params_from_reference
-from .env import VecMultiShipRLEnv
+from .env import LO_FIELDS, VecMultiShipRLEnv
 from .scenario import Scenario, polygons
 from .status import status_string
 from .trajectory import LOG_KEYS, REWARD_SERIES
@@ -295,7 +295,7 @@ class _View:
 
 def _real(field, scale=1.0):
     """A ship-state real [2, n_env] as a float attribute (scaled on read, divided on write)."""
-    return (lambda env, t: float(env._state()[field][t, 0]) * scale,
+    return (lambda env, t: env._read(field, t) * scale,
             lambda env, t, v: env._write(field, t, float(v) / scale))
 
 
@@ -598,7 +598,7 @@ class MultiShipRLEnv:
             self.time_since_last_ship_drawing += self._dt
         if self.record:
             st = self._host_state
-            self._rows.append((self._log.copy(), float(st["e_ct_int"][0, 0]), float(st["e_ct_int"][1, 0]),
+            self._rows.append((self._log.copy(), self._read("e_ct_int", 0), self._read("e_ct_int", 1),
                                self._obs_stop_pre))
             self._obs_stop_pre = bool(st["stop"][1, 0])
         self.state = next_state
@@ -643,18 +643,38 @@ class MultiShipRLEnv:
             self._cache = self._host_state
         return self._cache
 
+    def _read(self, field, t=None):
+        """One state real as a Python float: ship field [t, 0] or env field [0].  A float32 handle's
+        double-float fields (env.LO_FIELDS) are read as hi + lo, the value the kernel's decisions use."""
+        st = self._state()
+        idx = (0,) if t is None else (t, 0)
+        v = float(st[field][idx])
+        lo = LO_FIELDS.get(field)
+        if self._rs == 4 and lo is not None and lo in st:
+            v += float(st[lo][idx])
+        return v
+
     def _write(self, field, t, value):
-        """Write one ship's state field (the reference's attribute assignment) to the device."""
-        v = self._state()[field].copy()
+        """Write one ship's state field (the reference's attribute assignment) to the device.  A float32
+        handle's double-float field is written as hi = float32(value), lo = value - hi, the other ship's
+        hi + lo kept as they are."""
+        st = self._state()
+        v = st[field].copy()
         v[t, 0] = value
-        self.vec.set_state({field: v})
+        upd = {field: v}
+        lo = LO_FIELDS.get(field)
+        if lo is not None and lo in st:
+            vl = st[lo].copy()
+            vl[t, 0] = float(value) - float(np.float32(value)) if self._rs == 4 else 0.0
+            upd[lo] = vl
+        self.vec.set_state(upd)
         self._cache = None
         if field == "stop" and t == 1:
             self._obs_stop_pre = bool(value)
 
     @property
     def sampling_distance_travelled(self):
-        return float(self._state()["sampling_dist"][0])
+        return self._read("sampling_dist")
 
     @property
     def eps_distance_travelled(self):

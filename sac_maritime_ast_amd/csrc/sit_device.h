@@ -182,18 +182,27 @@ constexpr int kMaxPolys = 32;
 // math overloads
 // --------------------------------------------------------------------------------------
 // float32 sine / cosine (the heading's every step, the IW direction): the hardware's v_sin / v_cos
-// (argument scaled to revolutions; ~1e-6 absolute, within the float32 handle's 1e-5 contract) instead of
+// (argument scaled to revolutions; error measured and bounded by a GPU test) instead of
 // the library's range-reduced polynomial: C3 +2.9 %, C5 +1.6 % in same-box A/Bs, float32 drift
 // unchanged.  0: sincosf.  The float64 handle keeps the library's sin / cos.
 #ifndef SIT_FAST_TRIG
 #define SIT_FAST_TRIG 1
 #endif
 #if SIT_FAST_TRIG
-// v_sin / v_cos take the angle in revolutions and only |x / 2 pi| <= 256: the argument is scaled once
-// and reduced to [0, 1) with v_fract (exact), so any heading is valid; the scaling's float32 rounding
-// (~3e-8 relative of x) is below the float32 heading's own storage rounding at every magnitude
+// v_sin / v_cos take the angle in revolutions and only |x / 2 pi| <= 256.  The argument is scaled to
+// revolutions in two parts, t = x * c_hi and its rounding error e = fma(x, c_hi, -t) + x * c_lo
+// (c_hi + c_lo = 1 / 2 pi to ~2^-48), and reduced to [-0.5, 0.5] as (t - rint(t)) + e: t - rint(t) is
+// exact, so the revolution carries no error of its own at any heading (the reference does not wrap
+// headings, Q4).  Round to nearest, not v_fract: fract maps a small negative t to 1 - |t|, whose
+// float32 grid (6e-8 rev) is far coarser than t's own.  What remains is the instructions' own error,
+// measured and bounded by tests/test_gpu_parity.py::test_f32_fast_trig_accuracy (sit_selftest_f64
+// ops 9-10; profiles/r06_f32_trig_accuracy.json).
 __device__ __forceinline__ void xsincos(float x, float* s, float* c) {
-  const float rev = __builtin_amdgcn_fractf(x * 0.159154943091895336f);
+#pragma clang fp reassociate(off) contract(off)
+  constexpr float kRevHi = 0.15915493667125702f, kRevLo = 6.420638e-09f;
+  const float t = x * kRevHi;
+  const float e = __builtin_fmaf(x, kRevHi, -t) + x * kRevLo;
+  const float rev = (t - __builtin_rintf(t)) + e;
   *s = __builtin_amdgcn_sinf(rev);
   *c = __builtin_amdgcn_cosf(rev);
 }
@@ -568,6 +577,9 @@ __device__ __forceinline__ T comp_fma(T hi, T& lo, T a, T b) {
 #ifndef SIT_COMP_PI
 #define SIT_COMP_PI 1    // the heading PID and the ship-speed PI integrals
 #endif
+#ifndef SIT_PID_ERR_LO
+#define SIT_PID_ERR_LO 1 // the heading PID's error from the heading's hi + lo (0: from hi alone)
+#endif
 template <bool ON, typename T>
 __device__ __forceinline__ T comp_fma_if(T hi, T& lo, T a, T b) {
   if constexpr (ON) return comp_fma(hi, lo, a, b);
@@ -682,8 +694,10 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
   const T chi = xatan(-q - s.ect_int * c.los_ki);
   const T psi_ref = alpha + chi;
   psi_ref_out = psi_ref;
-  // heading PID, error not wrapped (Q4)
-  const T err = psi_ref - s.psi;
+  // heading PID, error not wrapped (Q4).  float32: the heading's double-float value psi + lpsi (the low
+  // part is a bias that changes slowly along a leg, and the PID integral would accumulate it)
+  T err = psi_ref - s.psi;
+  if constexpr (kComp<T> && SIT_PID_ERR_LO) err -= s.lpsi;
   const T derr = (err - s.hp) * c.inv_dt;
   s.hi = comp_fma_if<SIT_COMP_PI != 0>(s.hi, s.lhi, err, c.dt);
   s.hp = err;

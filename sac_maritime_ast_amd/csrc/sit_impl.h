@@ -1181,6 +1181,17 @@ __global__ __launch_bounds__(256) void k_selftest_f64(int op, int n, const doubl
     case 5: r = sin(x); break;            // the transcendental functions the float64 path and the
     case 6: r = cos(x); break;            // knife-edge re-evaluations call (ocml): compared with
     case 7: r = atan2(x, y); break;       // the reference's libm in tests/test_gpu_parity.py
+    // the float32 functions of the float32 step (this TU's build flags): the heading / IW-direction
+    // sine and cosine (xsincos: v_sin / v_cos under SIT_FAST_TRIG), the LOS course (atan) and the leg
+    // angle (atan2) of float32 arguments, returned as float64 (test_f32_fast_trig_accuracy)
+    case 9: case 10: {
+      float sf, cf;
+      xsincos((float)x, &sf, &cf);
+      r = op == 9 ? (double)sf : (double)cf;
+      break;
+    }
+    case 11: r = (double)xatan((float)x); break;
+    case 12: r = (double)xatan2((float)x, (float)y); break;
     default: {                            // 8: k_env_steps_sync's roles for the SIMD assignment x
       // (base 4: SIMD of wave v = digit v) and CU ticket y: role of wave v in base-4 digit v
       const int s = (int)x, tk = (int)y;
@@ -1200,9 +1211,11 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_policy_apply(int cap, const T* head, int head_stride, const T* noise,
                                                       const int32_t* req_env, const int32_t* req_count,
                                                       int deterministic, T* policy_action, int32_t* policy_ready,
-                                                      int n_env) {
+                                                      unsigned long long* served, int n_env) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cap || i >= *req_count) return;
+  const int cnt = *req_count;
+  if (i == 0 && served) atomicAdd(served, (unsigned long long)(cnt < cap ? cnt : cap));
+  if (i >= cap || i >= cnt) return;
   const int e = req_env[i];
   if (e < 0 || e >= n_env) return;
   const T mu = head[(size_t)i * head_stride];

@@ -69,7 +69,7 @@ int sit_probe_map(sit_handle* h, int32_t n, const void* pts_ne, void* dist, uint
 
 int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, double* out, int32_t fast_tu,
                      void* stream) {
-  if (op < 0 || op > 8 || n < 0 || (n > 0 && (!a || !b || !out))) return SIT_E_INVALID;
+  if (op < 0 || op > 12 || n < 0 || (n > 0 && (!a || !b || !out))) return SIT_E_INVALID;
   if (n == 0) return SIT_OK;
   return fast_tu ? launch_selftest_f32tu(op, n, a, b, out, stream)
                  : launch_selftest(op, n, a, b, out, (hipStream_t)stream);
@@ -77,7 +77,7 @@ int sit_selftest_f64(int32_t op, int32_t n, const double* a, const double* b, do
 
 int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t head_stride, const void* noise,
                      const int32_t* request_env, const int32_t* request_count, int32_t deterministic,
-                     void* policy_action, int32_t* policy_ready, void* stream) {
+                     void* policy_action, int32_t* policy_ready, int64_t* served, void* stream) {
   if (!h) return fail(nullptr, SIT_E_INVALID, "null handle");
   if (capacity <= 0 || !head || head_stride < 2 || !request_env || !request_count || !policy_action ||
       !policy_ready || (!deterministic && !noise))
@@ -86,11 +86,11 @@ int sit_policy_apply(sit_handle* h, int32_t capacity, const void* head, int32_t 
   if (h->precision == SIT_F64)
     hipLaunchKernelGGL(k_policy_apply<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, capacity,
                        (const double*)head, head_stride, (const double*)noise, request_env, request_count,
-                       deterministic, (double*)policy_action, policy_ready, h->n_env);
+                       deterministic, (double*)policy_action, policy_ready, (unsigned long long*)served, h->n_env);
   else
     hipLaunchKernelGGL(k_policy_apply<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, capacity,
                        (const float*)head, head_stride, (const float*)noise, request_env, request_count,
-                       deterministic, (float*)policy_action, policy_ready, h->n_env);
+                       deterministic, (float*)policy_action, policy_ready, (unsigned long long*)served, h->n_env);
   HIP_TRY(h, hipGetLastError());
   return SIT_OK;
 }

@@ -804,8 +804,15 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
 #ifndef SIT_SYNC_WAVES_PER_EU
 #define SIT_SYNC_WAVES_PER_EU 0
 #endif
+// SIT_F64_WAVES_PER_EU: the same for the float64 instantiations alone (they live in the strict TU,
+// sit_kernels.hip, built with SIT_F32_TU defined; the float32 ones in sit_steps_f32.hip)
+#ifndef SIT_F64_WAVES_PER_EU
+#define SIT_F64_WAVES_PER_EU 0
+#endif
 #if SIT_SYNC_WAVES_PER_EU > 0
 #define SIT_SYNC_OCC __attribute__((amdgpu_waves_per_eu(SIT_SYNC_WAVES_PER_EU, SIT_SYNC_WAVES_PER_EU)))
+#elif SIT_F64_WAVES_PER_EU > 0 && defined(SIT_F32_TU)
+#define SIT_SYNC_OCC __attribute__((amdgpu_waves_per_eu(SIT_F64_WAVES_PER_EU, SIT_F64_WAVES_PER_EU)))
 #else
 #define SIT_SYNC_OCC
 #endif

@@ -111,6 +111,10 @@ def pack_actor_weights(policy: nn.Module, out: torch.Tensor | None = None) -> to
             return torch.cat([t.detach().to(torch.float32).reshape(-1) for t in parts]).contiguous()
         # in place, one copy per parameter into its segment of the block (no concatenated temporary:
         # half the host work of a refresh after each optimizer step)
+        if out.numel() != _lib.SIT_ACTOR_WEIGHTS or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError(f"pack_actor_weights: out must be a contiguous float32 tensor of "
+                             f"{_lib.SIT_ACTOR_WEIGHTS} elements (got {tuple(out.shape)} {out.dtype}, "
+                             f"contiguous={out.is_contiguous()})")
         o = 0
         for t, shape in ((l1.weight, (H, _lib.SIT_OBS_DIM)), (l1.bias, (H,)), (l2.weight.t(), (H, H)), (l2.bias, (H,)),
                          (l3.weight, (2, H)), (l3.bias, (2,))):
@@ -118,6 +122,26 @@ def pack_actor_weights(policy: nn.Module, out: torch.Tensor | None = None) -> to
             out[o:o + n].view(shape).copy_(t.detach())
             o += n
         return out
+
+
+def _trunk(net: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """net(x) for an nn.Sequential trunk, each Linear followed by a ReLU evaluated as one GEMM with
+    the bias and the ReLU in its epilogue (torch._addmm_activation: hipBLASLt's fused epilogue on ROCm)
+    instead of a GEMM and a separate elementwise kernel; any other layer as itself."""
+    layers = list(net) if isinstance(net, nn.Sequential) else None
+    if layers is None or x.dim() != 2 or not hasattr(torch, "_addmm_activation"):
+        return net(x)
+    i = 0
+    while i < len(layers):
+        m = layers[i]
+        if (isinstance(m, nn.Linear) and m.bias is not None and i + 1 < len(layers)
+                and isinstance(layers[i + 1], nn.ReLU)):
+            x = torch._addmm_activation(m.bias, x, m.weight.t())
+            i += 2
+        else:
+            x = m(x)
+            i += 1
+    return x
 
 
 class PolicySampler:
@@ -140,8 +164,12 @@ class PolicySampler:
     def __init__(self, env: VecMultiShipRLEnv, policy: nn.Module, chunk: int = 32, seed: int = 25450,
                  env_id_offset: int = 0, request_capacity: int | None = None, mask_horizon: int = 600,
                  transition_capacity: int = 0, deterministic: bool = False, actor_dtype=None,
-                 fused_actor: bool = True, serve: str | None = None):
+                 fused_actor: bool = True, serve: str | None = None, actor_stream: bool = False):
         self.env, self.policy, self.chunk, self.seed = env, policy, int(chunk), int(seed)
+        # queue serving: the actor on a HIP stream of its own, forked after the env launch and joined
+        # before the next (north_star's "actor forward interleaved with the HIP env step on separate
+        # streams"; with one group the two kernels still run in order: the next launch needs the actions)
+        self.actor_stream = torch.cuda.Stream(device=env.device) if actor_stream else None
         self.env_id_offset, self.mask_horizon = int(env_id_offset), int(mask_horizon)
         self.transition_capacity, self.deterministic = int(transition_capacity), deterministic
         n, dev, dt = env.n_env, env.device, env.dtype
@@ -220,7 +248,14 @@ class PolicySampler:
         if events is not None:
             events[1].record(torch.cuda.current_stream(self.env.device))
         if self.serve == "queue":
-            self.act()
+            if self.actor_stream is None:
+                self.act()
+            else:
+                cur = torch.cuda.current_stream(self.env.device)
+                self.actor_stream.wait_stream(cur)
+                with torch.cuda.stream(self.actor_stream):
+                    self.act()
+                cur.wait_stream(self.actor_stream)
         return self.out
 
     def capture(self, n_launch: int = 2, want=("next_state", "reward", "done", "status", "action")):
@@ -265,7 +300,7 @@ class PolicySampler:
         obs = io["request_obs"] if self.actor_dtype == env.dtype else io["request_obs"].to(self.actor_dtype)
         net = getattr(self.policy, "net", None)
         if net is not None and getattr(self.policy, "act_dim", 1) == 1:
-            head = net(obs)
+            head = _trunk(net, obs)
             if head.dtype != env.dtype:
                 head = head.to(env.dtype)
             head = head.contiguous()
@@ -273,15 +308,16 @@ class PolicySampler:
                 env._call("sit_policy_apply", int(self._rows.numel()), head.data_ptr(), int(head.shape[1]),
                           io["request_noise"].data_ptr(), io["request_env"].data_ptr(),
                           io["request_count"].data_ptr(), int(bool(self.deterministic)),
-                          io["policy_action"].data_ptr(), io["policy_ready"].data_ptr(), env._stream())
-        else:
-            count = io["request_count"].clamp(max=self._rows.numel())
-            idx = torch.where(self._rows < count, io["request_env"], env.n_env).long()
-            action, _, _, _ = self.policy(obs, io["request_noise"].to(self.actor_dtype),
-                                          deterministic=self.deterministic)
-            io["policy_action"].index_put_((idx,), action[:, 0].to(io["policy_action"].dtype))
-            io["policy_ready"].index_put_((idx,), self._one)
-        self.served += io["request_count"].clamp(max=self._rows.numel())
+                          io["policy_action"].data_ptr(), io["policy_ready"].data_ptr(), self.served.data_ptr(),
+                          env._stream())
+            return
+        count = io["request_count"].clamp(max=self._rows.numel())
+        idx = torch.where(self._rows < count, io["request_env"], env.n_env).long()
+        action, _, _, _ = self.policy(obs, io["request_noise"].to(self.actor_dtype),
+                                      deterministic=self.deterministic)
+        io["policy_action"].index_put_((idx,), action[:, 0].to(io["policy_action"].dtype))
+        io["policy_ready"].index_put_((idx,), self._one)
+        self.served += count
 
 
 class OverlappedPolicySampler:

@@ -62,6 +62,12 @@ class TransitionGather:
         return sum(max(0, c - self.capacity) for c in self.host_counts)
 
 
+def _peer(group, r):
+    """The global rank of group rank r: torch.distributed's P2POp takes global peer ranks, while
+    rank / dst / world here count within `group`."""
+    return r if group is None else dist.get_global_rank(group, r)
+
+
 def _p2p_ops(rank, dst, world, counts, capacity, send, recv, group):
     """Point-to-point ops moving each rank's valid records (counts[r], clamped to the capacity) to
     rank dst.  Sizes are known on every rank, so every send has its matching receive."""
@@ -70,11 +76,11 @@ def _p2p_ops(rank, dst, world, counts, capacity, send, recv, group):
         for r in range(world):
             n = min(counts[r], capacity)
             if r != dst and n > 0:
-                ops.append(dist.P2POp(dist.irecv, recv[r][:n], r, group))
+                ops.append(dist.P2POp(dist.irecv, recv[r][:n], _peer(group, r), group))
     else:
         n = min(counts[rank], capacity)
         if n > 0:
-            ops.append(dist.P2POp(dist.isend, send[:n].contiguous(), dst, group))
+            ops.append(dist.P2POp(dist.isend, send[:n].contiguous(), _peer(group, dst), group))
     return ops
 
 
@@ -247,9 +253,11 @@ class TrajectoryGather:
                 if self.rank == self.dst:
                     for r in range(self.world):
                         if r != self.dst:
-                            ops += [dist.P2POp(dist.irecv, self.recv[f][r], r, self.group) for f in self.FIELDS]
+                            ops += [dist.P2POp(dist.irecv, self.recv[f][r], _peer(self.group, r), self.group)
+                                    for f in self.FIELDS]
                 else:
-                    ops += [dist.P2POp(dist.isend, self.send[f], self.dst, self.group) for f in self.FIELDS]
+                    ops += [dist.P2POp(dist.isend, self.send[f], _peer(self.group, self.dst), self.group)
+                            for f in self.FIELDS]
             self.work = dist.batch_isend_irecv(ops) if ops else []
             if self.rank == self.dst:
                 for f in self.FIELDS:

@@ -16,7 +16,7 @@ def test_algorithmic_bytes_per_env_step_rollout():
 
 
 def test_cpu_baseline_workers_report():
-    r = bench.cpu_baseline(0.5, 25450, 2)
+    r = bench.cpu_baseline(0.5, 25450, 3)     # 2 vectorised workers + the scalar loop, concurrently
     assert r["kind"] == "port" and r["unit"] == "env-steps/s"
     assert r["cores"] == 2 and r["value"] > 0 and r["per_core_value"] > 0
     assert "2 single-threaded processes" in r["sample"]

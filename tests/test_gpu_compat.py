@@ -257,6 +257,32 @@ def test_reference_constructor_float32_and_space_api():
     assert env.ship_model.int.time == env.test.ship_model.int.time == 300 * 0.5
 
 
+def test_float32_attribute_write_keeps_double_float_parts():
+    """On a float32 drop-in, the reference-style attribute assignment of one ship's double-float field
+    (``test.ship_model.north = x``) writes that ship's value as hi + lo = x (to the 48 bits two float32
+    parts hold) and leaves the other
+    ship's hi and lo untouched; the getters read hi + lo (the value the kernel's decisions use)."""
+    d = golden("env_nominal")
+    env = MultiShipRLEnv(fixture_assets(d), polygon_obstacle(), False, 30, ref_args(), device=DEV, precision=32,
+                         wpt_capacity=d["routes"].shape[1], record=False)
+    env.reset()
+    env.init_step()
+    for i in range(50):     # the integrators carry nonzero low parts after a few steps
+        env.step((d["action_n"][i], d["action_e"][i]), bool(d["sac_update"][i]), bool(d["init"][i]))
+    before = {k: v.cpu().numpy().copy() for k, v in env.vec.get_state().items()}
+    assert np.any(before["north_lo"] != 0)
+    x = 1234.567890123
+    env.test.ship_model.north = x
+    after = {k: v.cpu().numpy() for k, v in env.vec.get_state().items()}
+    assert after["north"][1, 0] == before["north"][1, 0] and after["north_lo"][1, 0] == before["north_lo"][1, 0]
+    # (hi + lo of two float32 values carries 48 bits: x to ~1e-12 m)
+    assert abs(float(after["north"][0, 0]) + float(after["north_lo"][0, 0]) - x) <= 1e-11
+    assert abs(env.test.ship_model.north - x) <= 1e-11 and after["north"][0, 0] == np.float32(x)
+    assert env.obs.ship_model.north == float(before["north"][1, 0]) + float(before["north_lo"][1, 0])
+    comb = env.vec.get_state(combined=True)
+    assert env.sampling_distance_travelled == float(comb["sampling_dist"][0].item())
+
+
 @pytest.mark.parametrize("record", [True, False])
 def test_drop_in_step_kernel(record):
     """Which step kernel the scalar drop-in runs (sit_step_kernel): a recording env (the default; its

@@ -9,6 +9,7 @@ Contract:
     (per-field floors); discrete outputs identical except where the oracle's own decision
     margin lies inside the float32 band (counted and bounded).
 """
+import json
 import os
 import sys
 
@@ -486,8 +487,9 @@ def test_f32_synthetic_rollout_step_vs_oracle():
 
 def test_f32_free_running_within_storage_bound():
     """float32 free-running against float64 from identical starts, 4096 envs x 2000
-    steps of the synthetic sampler with auto-reset, one step per launch (tools/f32_drift.py).  A third
-    run, the float64 kernel with its state rounded to float32 after every step, isolates what float32
+    steps of the synthetic sampler with auto-reset, one step per launch (tools/f32_drift.py), and the
+    same episodes as the bench runs them (fused 200-step launches), bit for bit equal to the one-step
+    run.  A third run, the float64 kernel with its state rounded to float32 after every step, isolates what float32
     state STORAGE alone costs.  Per env the runs are compared until the first step whose discrete
     outcome differs (done, status, sampling event, waypoint index, route length, stop flags, episode
     step, sampler counter).  Gated: before divergence the next_state deviation (per-field floors) is
@@ -501,7 +503,16 @@ def test_f32_free_running_within_storage_bound():
     arithmetic)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import f32_drift
-    rep = f32_drift.measure(4096, 2000, 77, log=False, attribute=True)
+    rep = f32_drift.measure(4096, 2000, 77, log=False, attribute=True, fused_chunk=200)
+    rec = os.environ.get("SIT_TEST_RECORD_DIR")
+    if rec:
+        with open(os.path.join(rec, "f32_flip_attribution.json"), "w") as f:
+            json.dump(rep, f, indent=1)
+    # the benchmarked instantiation (fused 200-step launches, LDS-staged map, transitions written) gives
+    # the one-step run's outputs and states bit for bit, so every bound below holds for it
+    fz = rep["fused"]
+    assert fz["kernel"].startswith("k_env_steps_sync<float") and "map=LDS" in fz["kernel"], fz["kernel"]
+    assert fz["envs_differing_from_one_step_run"] == 0
     att = rep["f32_flip_attribution"]
     assert att["envs"] == rep["f32"]["envs_diverged"] and att["neither"] == 0
     for f in att["flips"]:
@@ -525,6 +536,10 @@ def test_f32_free_running_within_storage_bound():
     assert f32["next_state_max"] <= 1e-5
     assert f32["next_state_max"] <= s32["next_state_max"]
     assert f32["envs_diverged"] <= 0.0025 * 4096
+    # every real state field of both ships (pose, velocities, shaft speed, the PI / PID / LOS integrals, the
+    # previous heading error) within the same 1e-5 before divergence
+    worst = max(f32["state_per_field_max"], key=f32["state_per_field_max"].get)
+    assert f32["state_per_field_max"][worst] <= 1e-5, f32["state_per_field_max"]
 
 
 # ------------------------------------------------------------------------------------------
@@ -611,6 +626,65 @@ def test_device_transcendentals_vs_reference_libm(fast_tu):
         report[fn.__name__] = (int((ulps == 0).sum()), len(a), int(ulps.max()))
         assert ulps.max() <= 2, f"{fn.__name__}: {int(ulps.max())} ulp"
     print("device vs reference libm (exact, total, max ulp):", report)
+
+
+# measured bound of the float32 step's sine / cosine (v_sin / v_cos of t - rint(t), t = x / 2 pi;
+# csrc/sit_device.h xsincos) against float64 sin / cos of the same float32 argument
+F32_TRIG_ABS_BOUND = 4e-7
+
+
+def test_f32_fast_trig_accuracy():
+    """The float32 step's heading / IW-direction sine and cosine (xsincos in the fast-math TU:
+    ship_model.py:248-250, the kinematics of both ships every step; LOS_guidance.py:110-113 and the
+    IW direction) against float64 sin / cos of the same float32 argument, over both ships' heading
+    ranges: |psi| <= 0.1 densely (the obstacle ship starts at psi = -0.0156), [-pi, pi] and unwrapped
+    headings to +-50 rad (the reference does not wrap, Q4).  Asserts the maximum absolute error; reports
+    it, the error relative to |sin psi| where |sin psi| >= 1e-3, and, near psi = 0, the error in units
+    of the float32 ulp of psi.  Also the float32 atan (the LOS course) and atan2 (the leg angle) in
+    ulps of their float64 value."""
+    rng = np.random.default_rng(11)
+    dense = np.linspace(-0.1, 0.1, 400_001)
+    tiny = np.concatenate([-np.logspace(-9, -1, 4000), np.logspace(-9, -1, 4000), [0.0, -0.0156, -0.0156123]])
+    sets = {"|psi|<=0.1": np.concatenate([dense, tiny]), "[-pi,pi]": rng.uniform(-np.pi, np.pi, 1 << 18),
+            "+-50 rad": rng.uniform(-50, 50, 1 << 18)}
+    lib = _lib.load()
+
+    def run(op, a, b=None):
+        ta = torch.from_numpy(a).to(DEV)
+        tb = torch.from_numpy(a if b is None else b).to(DEV)
+        out = torch.empty_like(ta)
+        _lib.check(lib.sit_selftest_f64(op, len(a), ta.data_ptr(), tb.data_ptr(), out.data_ptr(), 1, None))
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+    report = {}
+    worst = 0.0
+    for name, x in sets.items():
+        x = x.astype(np.float32).astype(np.float64)      # the float32 argument, exactly
+        s, c = run(9, x), run(10, x)
+        es, ec = np.abs(s - np.sin(x)), np.abs(c - np.cos(x))
+        big = np.abs(np.sin(x)) >= 1e-3
+        r = {"max_abs_sin": float(es.max()), "max_abs_cos": float(ec.max()),
+             "max_rel_sin_where_|sin|>=1e-3": float((es[big] / np.abs(np.sin(x[big]))).max())}
+        if name == "|psi|<=0.1":
+            nz = np.abs(x) > 0
+            ulp = np.spacing(np.abs(x[nz]).astype(np.float32)).astype(np.float64)
+            r["max_sin_err_in_ulps_of_psi"] = float((es[nz] / ulp).max())
+        report[name] = r
+        worst = max(worst, r["max_abs_sin"], r["max_abs_cos"])
+    xs = rng.uniform(-20, 20, 1 << 16).astype(np.float32).astype(np.float64)
+    ua = np.abs(run(11, xs) - np.arctan(xs)) / np.spacing(np.abs(np.arctan(xs)).astype(np.float32)).astype(np.float64)
+    dy = rng.uniform(-1e4, 1e4, 1 << 16).astype(np.float32).astype(np.float64)
+    dx = rng.uniform(-1e4, 1e4, 1 << 16).astype(np.float32).astype(np.float64)
+    w = np.arctan2(dy, dx)
+    ub = np.abs(run(12, dy, dx) - w) / np.spacing(np.abs(w).astype(np.float32)).astype(np.float64)
+    report["atan_f32_max_ulp"], report["atan2_f32_max_ulp"] = float(ua.max()), float(ub.max())
+    print("float32 step trig vs float64:", report)
+    rec = os.environ.get("SIT_TEST_RECORD_DIR")
+    if rec:
+        with open(os.path.join(rec, "f32_trig_accuracy.json"), "w") as f:
+            json.dump(report, f, indent=1)
+    assert worst <= F32_TRIG_ABS_BOUND, f"float32 sin/cos error {worst:.3e} > {F32_TRIG_ABS_BOUND}"
+    assert report["atan_f32_max_ulp"] <= 4 and report["atan2_f32_max_ulp"] <= 4
 
 
 # ------------------------------------------------------------------------------------------

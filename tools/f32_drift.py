@@ -62,11 +62,16 @@ def _differs(a, b):
     return out
 
 
-def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False):
+def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False, fused_chunk=0):
     """The report (a dict) of n_env envs x steps steps; tests/test_gpu_parity.py gates on it.
     attribute: for every env at its first float32 divergence, re-run that step in float64 from the
     float32 run's own pre-step state (a float64 handle of the same envs and global ids, teacher-forced
-    for one step) and record which of the two decisions the exact arithmetic takes there."""
+    for one step) and record which of the two decisions the exact arithmetic takes there.
+    fused_chunk > 0: a fourth handle, float32, runs the same episodes as bench.py times them — fused
+    launches of `fused_chunk` steps (k_env_steps_sync with the LDS-staged map, replay transitions
+    written) — and every one of its steps' outputs and its state at every launch end are compared
+    bit for bit with the one-step-per-launch float32 run: where they are identical, the deviations
+    measured per step on the one-step run are those of the benchmarked instantiation."""
     args = argparse.Namespace(n_env=n_env, steps=steps, seed=seed)
     n = args.n_env
     sc = make_scenario(n, cap=48)
@@ -81,11 +86,28 @@ def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False):
     outs = {k: {} for k in envs}
     flips = []
     tf = VecMultiShipRLEnv(scenario=sc, precision=64, device="cuda:0") if attribute else None
+    fz = None
+    if fused_chunk:
+        fz = VecMultiShipRLEnv(scenario=sc, precision=32, device="cuda:0")
+        fz.reset()
+        fz.init_step()
+        fz_out, fz_rows, fz_bad = {}, [], np.zeros(n, dtype=bool)
+        fz_tcap = max(n, n * fused_chunk // 96)
+        fz_kernel = None
     for step in range(args.steps):
+        if fz is not None and step % fused_chunk == 0:
+            k = min(fused_chunk, args.steps - step)
+            o = fz.rollout(k, seed=args.seed, out=fz_out, transition_capacity=fz_tcap)
+            fz_kernel = fz.lib.sit_step_kernel(fz.handle).decode()
+            fz_rows = [{q: o[q][i].cpu().numpy() for q in ("next_state", "reward", "done", "status", "action")}
+                       for i in range(k)]
+            fz_state = {q: v.cpu().numpy() for q, v in fz.get_state().items()}
         res = {}
         pre = {k: state(envs[k]) for k in ("f32", "f64")} if attribute else None
         for k, e in envs.items():
             o = e.rollout(1, seed=args.seed, out=outs[k])
+            if k == "f32" and fz is not None:
+                e._last_rows = {q: o[q][0].cpu().numpy() for q in ("next_state", "reward", "done", "status", "action")}
             res[k] = ({q: o[q][0].cpu().numpy() for q in ("next_state", "reward", "done", "status")} |
                       {"sac": o["action"][0, :, 3].cpu().numpy()}, state(e))
         if attribute:
@@ -136,6 +158,21 @@ def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False):
                                                                SCALE[f]).max() for f in REAL)),
                         "hull": hull,
                     })
+        if fz is not None:
+            # the fused launch's row of this step against the one-step launch's, bit for bit
+            o1 = envs["f32"]._last_rows
+            row = fz_rows[step % fused_chunk]
+            for q in row:
+                a, b = row[q], o1[q]
+                eq = (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else a == b
+                fz_bad |= ~eq.reshape(n, -1).all(1)
+            if (step + 1) % fused_chunk == 0 or step + 1 == args.steps:
+                s1 = {q: v.cpu().numpy() for q, v in envs["f32"].get_state().items()}
+                for q, v in fz_state.items():
+                    if q.startswith("iw_key"):        # the single-step launches' IW-test cache, not model state
+                        continue
+                    d = v != s1[q]
+                    fz_bad |= d.reshape(-1, n).any(0) if d.ndim > 1 else d
         # s32: float32 state storage (every real field of the state rounded after the step)
         s = res["s32"][1]
         envs["s32"].set_state({f: v.astype(np.float32).astype(np.float64) for f, v in s.items()
@@ -159,6 +196,12 @@ def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False):
                   f"s32 {int((first['s32'] < args.steps).sum())}", file=sys.stderr, flush=True)
     report = {"what": __doc__.split("\n\n")[0], "n_env": n, "steps": args.steps,
               "kernel": envs["f32"].lib.sit_step_kernel(envs["f32"].handle).decode()}
+    if fz is not None:
+        report["fused"] = {"kernel": fz_kernel, "steps_per_launch": fused_chunk,
+                           "envs_differing_from_one_step_run": int(fz_bad.sum()),
+                           "how": "every step's outputs (next_state, reward, done, status, action) and the state at "
+                                  "every launch end of the fused float32 run, bit for bit against the one-step "
+                                  "float32 run"}
     for k, label in (("f32", "float32 kernel vs float64 kernel"), ("s32", "float32 state storage only")):
         div = first[k] < args.steps
         r = {"label": label, "envs_diverged": int(div.sum()),
@@ -195,8 +238,10 @@ def main():
     ap.add_argument("--seed", type=int, default=77)
     ap.add_argument("--out", default=None)
     ap.add_argument("--attribute", action="store_true", help="attribute every float32 divergence (see measure)")
+    ap.add_argument("--fused-chunk", type=int, default=0, help="> 0: also run the benchmarked instantiation "
+                    "(fused launches of this many steps) and compare it bit for bit with the one-step run")
     args = ap.parse_args()
-    report = measure(args.n_env, args.steps, args.seed, attribute=args.attribute)
+    report = measure(args.n_env, args.steps, args.seed, attribute=args.attribute, fused_chunk=args.fused_chunk)
     txt = json.dumps(report, indent=1)
     print(txt)
     if args.out:
