@@ -694,10 +694,18 @@ __device__ __forceinline__ void guidance_control(const C& c, const ConstsX64& x,
   const T chi = xatan(-q - s.ect_int * c.los_ki);
   const T psi_ref = alpha + chi;
   psi_ref_out = psi_ref;
-  // heading PID, error not wrapped (Q4).  float32: the heading's double-float value psi + lpsi (the low
-  // part is a bias that changes slowly along a leg, and the PID integral would accumulate it)
-  T err = psi_ref - s.psi;
-  if constexpr (kComp<T> && SIT_PID_ERR_LO) err -= s.lpsi;
+  // heading PID, error not wrapped (Q4).  float32: err = ((alpha - psi) - lpsi) + chi, not
+  // (alpha + chi) - psi: alpha - psi is exact (Sterbenz), so neither the float32 rounding of
+  // psi_ref = alpha + chi (up to 1.2e-7 rad, constant along a straight leg) nor the heading's low part
+  // enters err as a bias the PID integral would accumulate.  (Measured: the heading integral's float32
+  // deviation is not bounded by these biases but by the trajectory's own)
+  T err;
+  if constexpr (kComp<T> && SIT_PID_ERR_LO) {
+#pragma clang fp reassociate(off) contract(off)
+    err = ((alpha - s.psi) - s.lpsi) + chi;
+  } else {
+    err = psi_ref - s.psi;
+  }
   const T derr = (err - s.hp) * c.inv_dt;
   s.hi = comp_fma_if<SIT_COMP_PI != 0>(s.hi, s.lhi, err, c.dt);
   s.hp = err;

@@ -908,10 +908,18 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
     else if (prio[role] == 2) __builtin_amdgcn_s_setprio(2);
     else if (prio[role] == 3) __builtin_amdgcn_s_setprio(3);
   }
+#ifdef SIT_ONLY_ROLE   // diagnostic builds only (register report per role; results wrong): one role's code
+  if (SIT_ONLY_ROLE == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, pub, env, act);
+  else if (SIT_ONLY_ROLE == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, pub, env, act);
+  else if (SIT_ONLY_ROLE == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, pub, ring, env, act);
+  else sync_p<T, MODE, 1, LDSMAP>(a, cs, map, X, pub, ring, env, act);
+  (void)role;
+#else
   if (role == 0) sync_d<T, MODE, 0, MACH>(a, cs, X, pub, env, act);
   else if (role == 1) sync_d<T, MODE, 1, MACH>(a, cs, X, pub, env, act);
   else if (role == 2) sync_p<T, MODE, 0, LDSMAP>(a, cs, map, X, pub, ring, env, act);
   else sync_p<T, MODE, 1, LDSMAP>(a, cs, map, X, pub, ring, env, act);
+#endif
   if (MODE == kPolicy && pub) {
 #ifdef SIT_DIAG_SYNC
     const unsigned long long sy_s0 = __builtin_amdgcn_s_memtime();

@@ -14,6 +14,8 @@ O=gpurun_out/$T
 mkdir -p $O
 F64="--precision 64 --chunk 10000 --steps 30000 --warmup 40000 --no-c5"
 TORCH="--mode policy --serve queue --torch-actor --groups 2 --chunk 32 --steps 4096 --warmup 15360"
+# the c5_torch_actor line since round 6 (one group, 64-step launches, the actor on its own stream)
+TORCH1="--mode policy --serve queue --torch-actor --actor-stream --groups 1 --chunk 64 --steps 8192 --warmup 15360"
 case $P in
 a)
   tools/gpu_steps.sh \
@@ -44,6 +46,17 @@ c)
       --timeout 600 --timeout-method thread -s -k "fast_trig or free_running_within or float32_attribute or launch_partition" --- \
     $T/bench 300 python3 -u bench.py --- \
     $T/torch_sweep 600 bash tools/c5_torch_sweep.sh $O/c5t 1:64:3:1 1:64:6:1 1:64:8:1 1:80:4:1 1:64:4:1 ;;
+d)
+  tools/gpu_steps.sh \
+    $T/drift_main 300 python3 tools/f32_drift.py --out $O/drift_main.json --- \
+    $T/drift_alphacall 300 env SIT_LIBRARY=build_diag/libsit_alphacall.so python3 tools/f32_drift.py --out $O/drift_alphacall.json --- \
+    $T/drift_noalpha 300 env SIT_LIBRARY=build_diag/libsit_noalpha.so python3 tools/f32_drift.py --out $O/drift_noalpha.json --- \
+    $T/ab_c3 900 bash tools/ab_libs.sh 2 sac_maritime_ast_amd/libsit.so build_diag/libsit_alphacall.so build_diag/libsit_noalpha.so build_diag/libsit_prev.so --- \
+    $T/prof_torch1 300 rocprofv3 --kernel-trace --stats -d $O/prof_torch1 -o run --output-format csv -- python3 bench.py --no-cpu-baseline $TORCH1
+  rc=$?
+  [ -f $O/prof_torch1/run_kernel_trace.csv ] && python3 tools/trace_breakdown.py $O/prof_torch1/run_kernel_trace.csv > $O/torch1_breakdown.json
+  find $O -name "run_kernel_trace.csv" -delete
+  exit $rc ;;
 pmc64)
   tools/gpu_steps.sh $T/pmc_f64 900 bash tools/pmc.sh $O/pmc_f64 $F64
   rc=$?
