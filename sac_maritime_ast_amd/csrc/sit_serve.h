@@ -93,6 +93,9 @@ __device__ __forceinline__ float actor_head(float mu, float ls_raw, float noise,
 #define SIT_SERVE_ROWS 16
 #endif
 constexpr int kServeRows = SIT_SERVE_ROWS;   // request rows per pass of the block's actor (even)
+#ifndef SIT_SERVE_VAR
+#define SIT_SERVE_VAR 1   // passes of 4 / 8 / 12 / kServeRows rows by the rows left (0: always kServeRows)
+#endif
 #ifndef SIT_SERVE_KB
 #define SIT_SERVE_KB 8
 #endif
@@ -135,10 +138,13 @@ __host__ __device__ constexpr size_t serve_lds_bytes(size_t map_bytes) {
 // wave-uniform LDS broadcasts feeding packed FMAs), the two half sums combined in sit_policy_actor's
 // order ((q0 + q1) + (q2 + q3)) + b2, layer 3 by 16 lanes per (row, output).  Rows past `count` are
 // computed on whatever the published rows hold and never written.  Leaves (mu, log_sigma) in W.head.
+// R (even, <= kServeRows): the rows of this pass; each row's arithmetic is the same for every R.
+template <int R>
 __device__ __forceinline__ void serve_pass(const float* __restrict__ w, const ServePub& P, ServeWork& W, int row0,
                                            const float (&wr)[kActorObs], float b1, float b2) {
 #pragma clang fp reassociate(off) contract(off)
-  constexpr int H = kActorHidden, R = kServeRows, KB = kServeKB;
+  static_assert(R % 2 == 0 && R <= kServeRows, "pass rows");
+  constexpr int H = kActorHidden, KB = kServeKB;
   const int j = threadIdx.x, q = j >> 6, l = j & 63;
   // layer 1: h1 = relu(W1 obs + b1), one row pair at a time (unrolled over all rows, the compiler
   // held every row's observation in registers at once)
@@ -265,7 +271,18 @@ __device__ __forceinline__ void serve_block(const float* __restrict__ w, bool de
   for (int i = 0; i < kActorObs; ++i) wr[i] = w[kActorW1 + j * kActorObs + i];
   const float b1 = w[kActorB1 + j], b2 = w[kActorB2 + j];
   for (int row0 = 0; row0 < count; row0 += kServeRows) {
-    serve_pass(w, P, W, row0, wr, b1, b2);
+    // the pass sized to the rows left, rounded up to 4 (a block serves ~10 rows per 64-step launch at C5:
+    // a fixed 16-row pass computed ~35 % padding rows, and the pass is FLOP-bound)
+    const int rem = count - row0;
+#if SIT_SERVE_VAR
+    if (rem <= 4) serve_pass<4>(w, P, W, row0, wr, b1, b2);
+    else if (rem <= 8) serve_pass<8>(w, P, W, row0, wr, b1, b2);
+    else if (rem <= 12) serve_pass<12>(w, P, W, row0, wr, b1, b2);
+    else serve_pass<kServeRows>(w, P, W, row0, wr, b1, b2);
+#else
+    (void)rem;
+    serve_pass<kServeRows>(w, P, W, row0, wr, b1, b2);
+#endif
     if (j < kServeRows && row0 + j < count) {
       const int e = SIT_DCLAMP(P.env[row0 + j], n_env, kDbgServeEnv);
       policy_action[e] = (T)actor_head(W.head[2 * j], W.head[2 * j + 1], P.noise[row0 + j], deterministic);

@@ -932,6 +932,12 @@ __global__ __launch_bounds__(256) SIT_SYNC_OCC void k_env_steps_sync(const KArgs
     }
 #endif
     serve_block<T>(a.io.actor_w, a.io.actor_det != 0, smem, *pub, a.io.policy_action, a.io.actor_served, a.n_env);
+#ifdef SIT_ABL_SERVE_REPEAT   // timing ablation (served counts wrong): the serving pass run again, to price one
+    for (int rep = 1; rep < SIT_ABL_SERVE_REPEAT; ++rep) {   // more serving round per launch
+      __syncthreads();
+      serve_block<T>(a.io.actor_w, a.io.actor_det != 0, smem, *pub, a.io.policy_action, nullptr, a.n_env);
+    }
+#endif
 #ifdef SIT_DIAG_SYNC   // slot 14: the wait at barrier D and the serving (per launch)
     if (lane == 0) atomicAdd(&g_sit_diag[role >> 1][(role & 1) * 16 + 14], __builtin_amdgcn_s_memtime() - sy_s0);
 #endif

@@ -57,6 +57,31 @@ d)
   [ -f $O/prof_torch1/run_kernel_trace.csv ] && python3 tools/trace_breakdown.py $O/prof_torch1/run_kernel_trace.csv > $O/torch1_breakdown.json
   find $O -name "run_kernel_trace.csv" -delete
   exit $rc ;;
+e)
+  # C5 (in-kernel serving) launch length and the marginal cost of one serving round
+  for K in 32 64 128; do
+    timeout -k 10 200 python3 bench.py --mode policy --chunk $K --groups 1 --steps 8192 --warmup 30720 --no-cpu-baseline \
+      > $O/c5_k$K.json 2> $O/c5_k$K.err || exit 1
+  done
+  SIT_LIBRARY=build_diag/libsit_serve2.so timeout -k 10 200 python3 bench.py --mode policy --chunk 64 --groups 1 --steps 8192 \
+    --warmup 30720 --no-cpu-baseline > $O/c5_k64_serve2.json 2> $O/c5_k64_serve2.err || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c5 -o run --output-format csv -- python3 bench.py --mode policy \
+    --chunk 64 --groups 1 --steps 8192 --warmup 30720 --no-cpu-baseline > $O/prof_c5.log 2>&1 || exit 1
+  SIT_LIBRARY=build_diag/libsit_serve2.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c5_serve2 -o run \
+    --output-format csv -- python3 bench.py --mode policy --chunk 64 --groups 1 --steps 8192 --warmup 30720 --no-cpu-baseline \
+    > $O/prof_c5_serve2.log 2>&1 || exit 1
+  rm -f $O/prof_*/run_kernel_trace.csv
+  tools/gpu_steps.sh \
+    $T/tests 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -v --timeout 300 --timeout-method thread \
+      -k "launch_partition or equals_classic or f32_teacher_forced or synthetic_rollout or f32_rollout" --- \
+    $T/ab_c3 900 bash tools/ab_libs.sh 3 sac_maritime_ast_amd/libsit.so build_diag/libsit_nodist.so || exit $?
+  for f in $O/c5_k*.json; do python3 -c "
+import json; d=json.loads(open('$f').read().strip().splitlines()[-1])
+print('$f', '%.4e' % d['value'], 'frac %.3f' % d['config']['env_step_fraction'], 'launch ms %.4f' % d['roofline']['launch_ms']['median'])"; done ;;
+f)
+  tools/gpu_steps.sh \
+    $T/tests 600 python3 -u -m pytest tests/test_gpu_policy.py tests/test_gpu_debug.py -m gpu -v --timeout 300 --timeout-method thread --- \
+    $T/ab 900 bash tools/ab_libs.sh 3 sac_maritime_ast_amd/libsit.so build_diag/libsit_servefix.so ;;
 pmc64)
   tools/gpu_steps.sh $T/pmc_f64 900 bash tools/pmc.sh $O/pmc_f64 $F64
   rc=$?
