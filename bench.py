@@ -116,9 +116,10 @@ def algorithmic_bytes_per_launch(n_env, k, rs, mean_nw_obs, mean_nw_test, mode):
     return n_env * per_env
 
 
-def latest_pmc(precision, mode, n_env, chunk):
+def latest_pmc(precision, mode, n_env, chunk, serve="kernel"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this exact launch
-    configuration (precision, mode, envs, steps per launch), if any."""
+    configuration (precision, mode, envs, steps per launch; policy mode: in-kernel serving or the
+    request queue), if any; the newest round's file wins."""
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
@@ -126,7 +127,7 @@ def latest_pmc(precision, mode, n_env, chunk):
         except Exception:
             continue
         if (d.get("precision") == precision and d.get("mode") == mode and d.get("n_env") == n_env
-                and d.get("steps_per_launch") == chunk):
+                and d.get("steps_per_launch") == chunk and (mode != "policy" or d.get("serve", "kernel") == serve)):
             best = d
     return best
 
@@ -579,7 +580,7 @@ def bench_policy(args, rank, world, dev):
     kern_ms = float(np.median(launch_ms))
     rs = 4 if args.precision == 32 else 8
     alg = algorithmic_bytes_per_launch(per, chunk, rs, 3.0, 5.0, "rollout")
-    pmc = latest_pmc(args.precision, "policy", per, chunk)
+    pmc = latest_pmc(args.precision, "policy", per, chunk, args.serve)
     rl = roofline(alg, kern_ms, pmc, kern)
     rl["launch_ms"] = stats_of(launch_ms)
     rl["note"] = "per group launch (n_env / groups envs), groups run concurrently on separate streams"

@@ -82,6 +82,13 @@ f)
   tools/gpu_steps.sh \
     $T/tests 600 python3 -u -m pytest tests/test_gpu_policy.py tests/test_gpu_debug.py -m gpu -v --timeout 300 --timeout-method thread --- \
     $T/ab 900 bash tools/ab_libs.sh 3 sac_maritime_ast_amd/libsit.so build_diag/libsit_servefix.so ;;
+g)
+  # A/B of a variant against the main library (3 interleaved rounds), parity subset first
+  V=${3:-noahead}
+  tools/gpu_steps.sh \
+    $T/tests 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sim.py -m gpu -v --timeout 300 --timeout-method thread \
+      -k "launch_partition or equals_classic or f32_teacher_forced or synthetic_rollout or f32_rollout or free_running or knife or sim_" --- \
+    $T/ab 900 bash tools/ab_libs.sh 3 sac_maritime_ast_amd/libsit.so build_diag/libsit_$V.so build_diag/libsit_kb4.so ;;
 pmc64)
   tools/gpu_steps.sh $T/pmc_f64 900 bash tools/pmc.sh $O/pmc_f64 $F64
   rc=$?

@@ -15,6 +15,7 @@ ap.add_argument("--steps-per-launch", type=int, required=True)
 ap.add_argument("--n-env", type=int, default=32768)
 ap.add_argument("--precision", type=int, default=32)
 ap.add_argument("--mode", default="rollout")
+ap.add_argument("--serve", default="kernel", help="policy mode: kernel (in-kernel serving) or queue")
 ap.add_argument("--round", type=int, default=1)
 ap.add_argument("--source", default="")
 ap.add_argument("--kernel", default="k_env_steps_sync<float, 0> (D and P waves per ship, sit_sync.h)")
@@ -24,7 +25,7 @@ ws = d["SQ_WAVES"] * a.steps_per_launch
 keys = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_WR", "SQ_INSTS_VMEM_RD",
         "SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES", "SQ_LDS_BANK_CONFLICT",
         "SQ_INSTS_VALU_TRANS_F32")
-out = {"kernel": a.kernel, "precision": a.precision, "mode": a.mode,
+out = {"kernel": a.kernel, "precision": a.precision, "mode": a.mode, "serve": a.serve if a.mode == "policy" else None,
        "n_env": a.n_env, "steps_per_launch": a.steps_per_launch, "round": a.round, "source": a.source,
        "kernel_ns_per_launch": d["_ns"], "fetch_size_kb": d["FETCH_SIZE"], "write_size_kb": d["WRITE_SIZE"],
        "hbm_bytes_per_launch": (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024,
