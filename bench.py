@@ -527,19 +527,6 @@ def bench_policy(args, rank, world, dev):
                                       actor_stream=getattr(args, "actor_stream", False) and args.serve == "queue"))
     runner = OverlappedPolicySampler(samplers) if G > 1 else None
     cur = torch.cuda.current_stream(dev)
-    # kernel duration of the env launches: eager launches through the sampler (HIP events on each
-    # group's stream around the env kernel)
-    n_ev = 8
-    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
-          for _ in range(n_ev)]
-    for i in range(n_ev):
-        if runner:
-            runner.launch(events=ev[i])
-        else:
-            samplers[0].launch(events=ev[i][0])
-    torch.cuda.synchronize(dev)
-    launch_ms = [a.elapsed_time(b) for row in ev for a, b in row]
-    kern = kernel_name(samplers[0].env)
     # the timed loop: HIP-graph replays of `per_graph` launches of every group
     (runner or samplers[0]).capture(per_graph)
     n_rep = max(2, args.steps // (chunk * per_graph))
@@ -562,6 +549,22 @@ def bench_policy(args, rank, world, dev):
     for ga in gathers:
         ga.finish()
     torch.cuda.synchronize(dev)
+    # kernel duration of the env launches in the steady state (after the warm-up): eager launches through the
+    # sampler, HIP events on each group's stream around the env kernel (the timed replays are HIP graphs)
+    n_ev = 16
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
+          for _ in range(n_ev)]
+    for i in range(n_ev):
+        # the GPU kept busy while the host enqueues the launch (an eager launch otherwise starts after its start
+        # event by the host's enqueue time: the PyTorch-actor launch's ~20 us of Python)
+        torch.cuda._sleep(1_000_000)
+        if runner:
+            runner.launch(events=ev[i])
+        else:
+            samplers[0].launch(events=ev[i][0])
+    torch.cuda.synchronize(dev)
+    launch_ms = [a.elapsed_time(b) for row in ev for a, b in row]
+    kern = kernel_name(samplers[0].env)
     g0 = [(ga.gathered, ga.dropped()) for ga in gathers]
     before = sum(int(sm.env_steps.item()) for sm in samplers)
 
@@ -584,7 +587,8 @@ def bench_policy(args, rank, world, dev):
     rl = roofline(alg, kern_ms, pmc, kern)
     rl["launch_ms"] = stats_of(launch_ms)
     rl["note"] = "per group launch (n_env / groups envs), groups run concurrently on separate streams"
-    rl["kernel_ms_statistic"] = f"median over {n_ev * G} eager launches (HIP events on each group's stream)"
+    rl["kernel_ms_statistic"] = (f"median over {n_ev * G} eager launches after the warm-up (steady state; HIP events on "
+                                 f"each group's stream)")
     cfg = {"workload": "C5: 65 536 ships driven by the SAC-AST Gaussian policy (256x256 MLP, fp32, "
                        "evaluated in HIP for the envs waiting at each sampling event) and the HIP env step"
                        if world == 1 else

@@ -15,20 +15,21 @@ C3="--no-cpu-baseline --no-extra-lines --no-c5"
 C5="--no-cpu-baseline --mode policy --chunk 64 --groups 1 --steps 8192 --warmup 30720"
 F64="--no-cpu-baseline --no-extra-lines --no-c5 --precision 64 --chunk 10000 --steps 30000 --warmup 40000"
 TORCH="--no-cpu-baseline --mode policy --serve queue --torch-actor --actor-stream --groups 1 --chunk 64 --steps 8192 --warmup 15360"
-prof() {  # prof <name> <bench args>: kernel stats + the step kernel's dispatches (timed-launch average)
-  n=$1; shift
-  rocprofv3 --kernel-trace --stats -d $O/prof_$n -o run --output-format csv -- python3 bench.py "$@"
-}
+RP="rocprofv3 --kernel-trace --stats -o run --output-format csv"
 case $P in
 a)
   tools/gpu_steps.sh \
     $T/smoke 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" --- \
     $T/tests 900 env SIT_TEST_RECORD_DIR=$O python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -s --- \
-    $T/bench 400 python3 -u bench.py --- \
-    $T/prof_c3 300 prof c3 $C3 --- \
-    $T/prof_c5 300 prof c5 $C5 --- \
-    $T/prof_f64 300 prof f64 $F64 --- \
-    $T/prof_torch 300 prof torch $TORCH
+    $T/bench 400 python3 -u bench.py || exit $?
+  bash $0 $T p ;;
+p)
+  # rocprofv3 kernel stats + the step kernel's dispatches (timed-launch averages) of each line's launch shape
+  tools/gpu_steps.sh \
+    $T/prof_c3 300 $RP -d $O/prof_c3 -- python3 bench.py $C3 --- \
+    $T/prof_c5 300 $RP -d $O/prof_c5 -- python3 bench.py $C5 --- \
+    $T/prof_f64 300 $RP -d $O/prof_f64 -- python3 bench.py $F64 --- \
+    $T/prof_torch 300 $RP -d $O/prof_torch -- python3 bench.py $TORCH
   rc=$?
   for n in c3 c5 f64 torch; do
     f=$O/prof_$n/run_kernel_trace.csv
