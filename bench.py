@@ -109,10 +109,12 @@ def algorithmic_bytes_per_launch(n_env, k, rs, mean_nw_obs, mean_nw_test, mode):
     scen = 2 * 3 * rs + 2 * 8               # per env: end wpt + desired speed per ship, AB len/alpha
     routes = 2 * rs * ((mean_nw_obs - 1) * 2 + (mean_nw_test - 1))   # obs read+write back, test read
     out_step = 15 * rs + 1 + 4              # next_state 10 + reward + IW action 4, done u8, status u32
+    # float32: the double-float low parts, 11 per ship and 3 per env (csrc/sit_impl.h kShipLo / kEnvLo)
+    lo = (2 * 11 + 3) * rs if rs == 4 else 0
     if mode == "rollout":
-        per_env = 2 * (2 * ship_state + env_state) + scen + routes + k * out_step
+        per_env = 2 * (2 * ship_state + env_state + lo) + scen + routes + k * out_step
     else:  # per-step launch: state in and out every step, explicit action in
-        per_env = k * (2 * (2 * ship_state + env_state) + scen + 2 * rs * 3 + 2 * rs + 2 + out_step - 4 * rs)
+        per_env = k * (2 * (2 * ship_state + env_state + lo) + scen + 2 * rs * 3 + 2 * rs + 2 + out_step - 4 * rs)
     return n_env * per_env
 
 

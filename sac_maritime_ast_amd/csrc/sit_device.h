@@ -520,6 +520,7 @@ struct Ship {
   T lrpm, lect, lpme;        // last stored observations (stop path)
   // float32: the low parts of the integrators (comp_add): the value is n + ln etc.  float64: unused
   T ln, le, lpsi, li1, li2, lhi, lei;
+  T lu, lv, lr, lw;          // float32: the velocities' and the shaft speed's low parts (SIT_COMP_VEL / _W)
   int k;                     // next waypoint index
   int ticks;                 // simulator time in dt units
   int stop;                  // ShipAssets.stop_flag
@@ -576,6 +577,12 @@ __device__ __forceinline__ T comp_fma(T hi, T& lo, T a, T b) {
 #endif
 #ifndef SIT_COMP_PI
 #define SIT_COMP_PI 1    // the heading PID and the ship-speed PI integrals
+#endif
+#ifndef SIT_COMP_VEL
+#define SIT_COMP_VEL 1   // surge, sway and yaw rate (round 6)
+#endif
+#ifndef SIT_COMP_W
+#define SIT_COMP_W 1     // the shaft speed (the thrust force with the simplified machinery; round 6)
 #endif
 #ifndef SIT_PID_ERR_LO
 #define SIT_PID_ERR_LO 1 // the heading PID's error from the heading's hi + lo (0: from hi alone)
@@ -925,10 +932,10 @@ __device__ __forceinline__ void ship_dynamics_pos(const Consts<T>& c, Ship<T>& s
   s.ln = ln1;
   s.le = le1;
   s.psi = comp_fma_if<SIT_COMP_PSI != 0>(s.psi, s.lpsi, r, c.dt);
-  s.u = u + (c.inv_m11 * f0) * c.dt;
-  s.v = v + (c.inv_m22 * f1) * c.dt;
-  s.r = r + (c.inv_m33 * f2) * c.dt;
-  s.w = w + d_w * c.dt;
+  s.u = comp_fma_if<SIT_COMP_VEL != 0>(u, s.lu, c.inv_m11 * f0, c.dt);
+  s.v = comp_fma_if<SIT_COMP_VEL != 0>(v, s.lv, c.inv_m22 * f1, c.dt);
+  s.r = comp_fma_if<SIT_COMP_VEL != 0>(r, s.lr, c.inv_m33 * f2, c.dt);
+  s.w = comp_fma_if<SIT_COMP_W != 0>(w, s.lw, d_w, c.dt);
 }
 
 // ship_dynamics_pos in two parts with the same operations in the same order: DynBase holds every
@@ -991,10 +998,10 @@ __device__ __forceinline__ void dyn_finish(const C& c, Ship<T>& s, const DynBase
   s.ln = ln1;
   s.le = le1;
   s.psi = comp_fma_if<SIT_COMP_PSI != 0>(s.psi, s.lpsi, r, c.dt);
-  s.u = u + (c.inv_m11 * b.f0) * c.dt;
-  s.v = v + (c.inv_m22 * (b.f1 + f_rv)) * c.dt;
-  s.r = r + (c.inv_m33 * (b.f2 + f_rr)) * c.dt;
-  s.w = w + d_w * c.dt;
+  s.u = comp_fma_if<SIT_COMP_VEL != 0>(u, s.lu, c.inv_m11 * b.f0, c.dt);
+  s.v = comp_fma_if<SIT_COMP_VEL != 0>(v, s.lv, c.inv_m22 * (b.f1 + f_rv), c.dt);
+  s.r = comp_fma_if<SIT_COMP_VEL != 0>(r, s.lr, c.inv_m33 * (b.f2 + f_rr), c.dt);
+  s.w = comp_fma_if<SIT_COMP_W != 0>(w, s.lw, d_w, c.dt);
 }
 
 // --------------------------------------------------------------------------------------

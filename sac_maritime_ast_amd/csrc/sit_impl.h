@@ -80,6 +80,8 @@ const FieldSpec kFields[] = {
     {"yaw_lo", SIT_DT_REAL, kShip},       {"ship_speed_i_lo", SIT_DT_REAL, kShip},
     {"shaft_speed_i_lo", SIT_DT_REAL, kShip}, {"heading_i_lo", SIT_DT_REAL, kShip},
     {"e_ct_int_lo", SIT_DT_REAL, kShip},
+    {"surge_lo", SIT_DT_REAL, kShip},     {"sway_lo", SIT_DT_REAL, kShip},
+    {"yaw_rate_lo", SIT_DT_REAL, kShip},  {"shaft_speed_lo", SIT_DT_REAL, kShip},
     {"sampling_dist_lo", SIT_DT_REAL, kEnv},
     {"prev_pre_north_lo", SIT_DT_REAL, kEnv}, {"prev_pre_east_lo", SIT_DT_REAL, kEnv},
 };
@@ -87,9 +89,10 @@ constexpr int kNumFields = (int)(sizeof(kFields) / sizeof(kFields[0]));
 enum FieldId {
   F_NORTH = 0, F_LAST_PME = 14, F_K = 15, F_NW, F_TICKS, F_STOP,
   F_SAMP = 19, F_IW_E = 24, F_EP = 25, F_EVENT, F_EPISODES, F_WN, F_WE, F_LAST_OBS,
-  F_FUEL_ME, F_FUEL_EL, F_FUEL, F_LAST_LOG, F_IWK_N, F_IWK_E, F_IWK_FLAGS, F_SHIP_LO, F_ENV_LO = F_SHIP_LO + 7
+  F_FUEL_ME, F_FUEL_EL, F_FUEL, F_LAST_LOG, F_IWK_N, F_IWK_E, F_IWK_FLAGS, F_SHIP_LO, F_ENV_LO = F_SHIP_LO + 11
 };
-constexpr int kShipLo = 7;   // north, east, yaw, ship_speed_i, shaft_speed_i, heading_i, e_ct_int
+constexpr int kShipLo = 11;  // north, east, yaw, ship_speed_i, shaft_speed_i, heading_i, e_ct_int, surge, sway,
+                             // yaw_rate, shaft_speed
 // (the episode distance, which no decision or output reads, stays a plain float32 sum)
 constexpr int kEnvLo = 3;    // sampling_dist, prev_pre_north, prev_pre_east
 static_assert(F_ENV_LO + kEnvLo == kNumFields, "state field table and ids out of sync");
@@ -239,8 +242,10 @@ __device__ __forceinline__ void load_ship(const State<T>& st, int sid, Ship<T>& 
   if constexpr (kIsF32<T>) {
     s.ln = st.ship_lo[0][sid]; s.le = st.ship_lo[1][sid]; s.lpsi = st.ship_lo[2][sid];
     s.li1 = st.ship_lo[3][sid]; s.li2 = st.ship_lo[4][sid]; s.lhi = st.ship_lo[5][sid]; s.lei = st.ship_lo[6][sid];
+    s.lu = st.ship_lo[7][sid]; s.lv = st.ship_lo[8][sid]; s.lr = st.ship_lo[9][sid]; s.lw = st.ship_lo[10][sid];
   } else {
     s.ln = s.le = s.lpsi = s.li1 = s.li2 = s.lhi = s.lei = T(0);
+    s.lu = s.lv = s.lr = s.lw = T(0);
   }
 }
 
@@ -255,6 +260,7 @@ __device__ __forceinline__ void store_ship(const State<T>& st, int sid, const Sh
   if constexpr (kIsF32<T>) {
     st.ship_lo[0][sid] = s.ln; st.ship_lo[1][sid] = s.le; st.ship_lo[2][sid] = s.lpsi;
     st.ship_lo[3][sid] = s.li1; st.ship_lo[4][sid] = s.li2; st.ship_lo[5][sid] = s.lhi; st.ship_lo[6][sid] = s.lei;
+    st.ship_lo[7][sid] = s.lu; st.ship_lo[8][sid] = s.lv; st.ship_lo[9][sid] = s.lr; st.ship_lo[10][sid] = s.lw;
   }
 }
 
@@ -283,6 +289,9 @@ __device__ __forceinline__ void reset_ship(const Scen<T>& sc, int type, int env,
   s.ln = init_lo(sc, type, SIT_INIT_NORTH, env, n_env);
   s.le = init_lo(sc, type, SIT_INIT_EAST, env, n_env);
   s.lpsi = init_lo(sc, type, SIT_INIT_YAW, env, n_env);
+  s.lu = init_lo(sc, type, SIT_INIT_SURGE, env, n_env);
+  s.lv = init_lo(sc, type, SIT_INIT_SWAY, env, n_env);
+  s.lr = init_lo(sc, type, SIT_INIT_YAW_RATE, env, n_env);
   s.ect_int = T(0);
   s.lei = T(0);
   s.k = 1;
@@ -626,13 +635,13 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
   // construction pose, route length, first leg with its geometry, and initial observation.  Only
   // with auto-reset: a launch without it (sit_step, explicit actions) skips these loads and the
   // first leg's geometry in its prologue
-  T p0[6] = {}, p0lo[3] = {};
+  T p0[6] = {}, p0lo[6] = {};
   T lo0[6] = {};
   int nw0 = 0;
   typename Route<T>::Leg leg0{};
   if (act && __builtin_amdgcn_readfirstlane(a.io.auto_reset)) {
     for (int j = 0; j < 6; ++j) p0[j] = init_val(a.sc, type, SIT_INIT_NORTH + j, env, n_env);
-    for (int j = 0; j < 3; ++j) p0lo[j] = init_lo(a.sc, type, SIT_INIT_NORTH + j, env, n_env);
+    for (int j = 0; j < 6; ++j) p0lo[j] = init_lo(a.sc, type, SIT_INIT_NORTH + j, env, n_env);
     for (int j = 0; j < lo_n; ++j) lo0[j] = a.sc.initial_state[(size_t)env * SIT_OBS_DIM + lo_base + j];
     nw0 = a.sc.nw0[sid];
     Route<T> r0 = rt;
@@ -993,7 +1002,7 @@ __device__ __forceinline__ void env_steps(const KArgs<T>& a, unsigned char* smem
 #endif
         // reset() (MSRL_Env.py:147-188) from the register copies
         s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];
-        s.ln = p0lo[0]; s.le = p0lo[1]; s.lpsi = p0lo[2];
+        s.ln = p0lo[0]; s.le = p0lo[1]; s.lpsi = p0lo[2]; s.lu = p0lo[3]; s.lv = p0lo[4]; s.lr = p0lo[5];
         s.ect_int = T(0); s.lei = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
         rt.nw = nw0;
         rt.set_leg(leg0);
@@ -1237,6 +1246,7 @@ __global__ __launch_bounds__(256) void k_restart(const KArgs<T> a) {
     int nw;
     reset_ship(a.sc, type, env, n_env, s, nw);
     s.w = init_val(a.sc, type, SIT_INIT_SHAFT_SPEED, env, n_env);
+    s.lw = init_lo(a.sc, type, SIT_INIT_SHAFT_SPEED, env, n_env);
     s.i1 = init_val(a.sc, type, SIT_INIT_SHIP_SPEED_I, env, n_env);
     s.i2 = init_val(a.sc, type, SIT_INIT_SHAFT_SPEED_I, env, n_env);
     s.li1 = init_lo(a.sc, type, SIT_INIT_SHIP_SPEED_I, env, n_env);

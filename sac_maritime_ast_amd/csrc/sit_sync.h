@@ -226,13 +226,13 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
   };
   if (TYPE == 1 && act && (MODE == kSynth || (MODE == kPolicy && ready))) draw_next();
   if (MODE == kExplicit && TYPE == 1 && act && n > 0) load_inputs(0);
-  T p0[6] = {}, p0lo[3] = {};
+  T p0[6] = {}, p0lo[6] = {};
   int nw0 = 0;
   typename Route<T>::Leg leg0{};
   const bool auto_reset = __builtin_amdgcn_readfirstlane(a.io.auto_reset) != 0;
   if (act && auto_reset) {   // the episode start the auto reset restores (not loaded without it)
     for (int j = 0; j < 6; ++j) p0[j] = init_val(a.sc, TYPE, SIT_INIT_NORTH + j, env, n_env);
-    for (int j = 0; j < 3; ++j) p0lo[j] = init_lo(a.sc, TYPE, SIT_INIT_NORTH + j, env, n_env);
+    for (int j = 0; j < 6; ++j) p0lo[j] = init_lo(a.sc, TYPE, SIT_INIT_NORTH + j, env, n_env);
     nw0 = a.sc.nw0[sid];
     Route<T> r0 = rt;
     r0.nw = nw0;
@@ -421,7 +421,7 @@ __device__ __forceinline__ void sync_d(const KArgs<T>& a, const Consts<T>& cs, S
       if ((uf & kUfAutoReset) && env_done) {
         // reset() (MSRL_Env.py:147-188; shaft speed and every PI/PID integrator persist, Q6) + init_step()
         s.n = p0[0]; s.e = p0[1]; s.psi = p0[2]; s.u = p0[3]; s.v = p0[4]; s.r = p0[5];
-        s.ln = p0lo[0]; s.le = p0lo[1]; s.lpsi = p0lo[2];
+        s.ln = p0lo[0]; s.le = p0lo[1]; s.lpsi = p0lo[2]; s.lu = p0lo[3]; s.lv = p0lo[4]; s.lr = p0lo[5];
         s.ect_int = T(0); s.lei = T(0); s.k = 1; s.ticks = 0; s.stop = 0;
         rt.nw = nw0;
         rt.set_leg(leg0);

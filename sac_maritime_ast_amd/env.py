@@ -31,6 +31,7 @@ def _ptr(t):
 # reference integrates them in float64, and a float32 running sum loses up to half an ulp a step
 LO_FIELDS = {"north": "north_lo", "east": "east_lo", "yaw": "yaw_lo", "ship_speed_i": "ship_speed_i_lo",
              "shaft_speed_i": "shaft_speed_i_lo", "heading_i": "heading_i_lo", "e_ct_int": "e_ct_int_lo",
+             "surge": "surge_lo", "sway": "sway_lo", "yaw_rate": "yaw_rate_lo", "shaft_speed": "shaft_speed_lo",
              "sampling_dist": "sampling_dist_lo", "prev_pre_north": "prev_pre_north_lo",
              "prev_pre_east": "prev_pre_east_lo"}
 

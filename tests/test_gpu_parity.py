@@ -536,16 +536,14 @@ def test_f32_free_running_within_storage_bound():
     assert f32["next_state_max"] <= 1e-5
     assert f32["next_state_max"] <= s32["next_state_max"]
     assert f32["envs_diverged"] <= 0.0025 * 4096
-    # every real state field of both ships (pose, velocities, shaft speed, the PI / LOS integrals, the
-    # previous heading error) within the same 1e-5 before divergence.  The heading PID integral (the time
-    # integral of the heading error, which follows the trajectory's cross-track error through the LOS
-    # course) is held to what float32 state storage alone costs it: measured 1.4e-5 against 2.5e-5 / 5.7e-5
-    # for the storage-only run (profiles/r06_f32_flip_attribution.json)
-    sp, sp_s = f32["state_per_field_max"], s32["state_per_field_max"]
-    rest = {k: v for k, v in sp.items() if not k.startswith("heading_i")}
-    assert max(rest.values()) <= 1e-5, rest
-    for k in ("heading_i[0]", "heading_i[1]"):
-        assert sp[k] <= max(1e-5, sp_s[k]), (k, sp[k], sp_s[k])
+    # every real state field of both ships (pose, velocities, shaft speed, the PI / PID / LOS integrals, the
+    # previous heading error) within the same 1e-5 before divergence.  (The heading PID integral, the time
+    # integral of the heading error, follows the trajectory; it read 1.43e-5 until round 6 carried surge, sway,
+    # yaw rate and shaft speed as double-float values too: 7.0e-6, with 0 of 4 096 envs diverging,
+    # profiles/r06_heading_i_storage_attribution.json)
+    sp = f32["state_per_field_max"]
+    worst = max(sp, key=sp.get)
+    assert sp[worst] <= 1e-5, (worst, sp)
 
 
 # ------------------------------------------------------------------------------------------

@@ -62,7 +62,7 @@ def _differs(a, b):
     return out
 
 
-def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False, fused_chunk=0):
+def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False, fused_chunk=0, storage_fields=None):
     """The report (a dict) of n_env envs x steps steps; tests/test_gpu_parity.py gates on it.
     attribute: for every env at its first float32 divergence, re-run that step in float64 from the
     float32 run's own pre-step state (a float64 handle of the same envs and global ids, teacher-forced
@@ -71,7 +71,9 @@ def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False, fused_ch
     launches of `fused_chunk` steps (k_env_steps_sync with the LDS-staged map, replay transitions
     written) — and every one of its steps' outputs and its state at every launch end are compared
     bit for bit with the one-step-per-launch float32 run: where they are identical, the deviations
-    measured per step on the one-step run are those of the benchmarked instantiation."""
+    measured per step on the one-step run are those of the benchmarked instantiation.
+    storage_fields: round only these state fields to float32 in the storage-only run (an attribution of
+    the float32 run's deviations to the storage of individual fields; None = every real field)."""
     args = argparse.Namespace(n_env=n_env, steps=steps, seed=seed)
     n = args.n_env
     sc = make_scenario(n, cap=48)
@@ -176,7 +178,7 @@ def measure(n_env=4096, steps=2000, seed=77, log=True, attribute=False, fused_ch
         # s32: float32 state storage (every real field of the state rounded after the step)
         s = res["s32"][1]
         envs["s32"].set_state({f: v.astype(np.float32).astype(np.float64) for f, v in s.items()
-                               if v.dtype == np.float64})
+                               if v.dtype == np.float64 and (storage_fields is None or f in storage_fields)})
         ref_o, ref_s = res["f64"]
         for k in first:
             o, st = res[k]
@@ -240,8 +242,10 @@ def main():
     ap.add_argument("--attribute", action="store_true", help="attribute every float32 divergence (see measure)")
     ap.add_argument("--fused-chunk", type=int, default=0, help="> 0: also run the benchmarked instantiation "
                     "(fused launches of this many steps) and compare it bit for bit with the one-step run")
+    ap.add_argument("--storage-fields", default=None, help="comma-separated: the storage-only run rounds only these")
     args = ap.parse_args()
-    report = measure(args.n_env, args.steps, args.seed, attribute=args.attribute, fused_chunk=args.fused_chunk)
+    report = measure(args.n_env, args.steps, args.seed, attribute=args.attribute, fused_chunk=args.fused_chunk,
+                     storage_fields=args.storage_fields.split(",") if args.storage_fields else None)
     txt = json.dumps(report, indent=1)
     print(txt)
     if args.out:

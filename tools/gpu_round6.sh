@@ -89,6 +89,14 @@ g)
     $T/tests 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sim.py -m gpu -v --timeout 300 --timeout-method thread \
       -k "launch_partition or equals_classic or f32_teacher_forced or synthetic_rollout or f32_rollout or free_running or knife or sim_" --- \
     $T/ab 900 bash tools/ab_libs.sh 3 sac_maritime_ast_amd/libsit.so build_diag/libsit_$V.so build_diag/libsit_kb4.so ;;
+h)
+  V=${3:-nocompvel}
+  tools/gpu_steps.sh \
+    $T/drift 300 python3 tools/f32_drift.py --out $O/drift_main.json --- \
+    $T/drift_$V 300 env SIT_LIBRARY=build_diag/libsit_$V.so python3 tools/f32_drift.py --out $O/drift_$V.json --- \
+    $T/tests 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sim.py tests/test_gpu_compat.py tests/test_gpu_policy.py \
+      -m gpu -v --timeout 300 --timeout-method thread -x -k "not free_running_within" --- \
+    $T/ab 900 bash tools/ab_libs.sh 3 sac_maritime_ast_amd/libsit.so build_diag/libsit_$V.so ;;
 pmc64)
   tools/gpu_steps.sh $T/pmc_f64 900 bash tools/pmc.sh $O/pmc_f64 $F64
   rc=$?
