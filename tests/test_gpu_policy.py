@@ -828,3 +828,34 @@ def test_rollout_serving_argument_checks():
     assert "kPolicy" in env.lib.sit_step_kernel(env.handle).decode()
     # every env started at its episode's first sampling event with no action: served in the same launch
     assert (ready[:n] == _lib.SIT_POLICY_READY).all()
+
+
+def test_torch_actor_on_its_stream_matches_fused_actor():
+    """The PyTorch-ROCm actor as bench.py's c5_torch_actor line runs it — each hidden Linear + ReLU one GEMM
+    with the ReLU in its epilogue (samplers._trunk), the head and scatter in sit_policy_apply (which also
+    counts the served rows), the actor forked onto a HIP stream of its own after the launch and joined
+    before the next — against the fused HIP actor on the same request queue (float32, 1 024 envs): the
+    first launch stops every env at its episode's first sampling event, so both queues hold every env;
+    the actions agree within 1e-5 and the served counts are equal."""
+    n_env = 1024
+    pol = make_policy256(DEV)
+    out = []
+    for fused, stream in ((True, False), (False, True)):
+        env = VecMultiShipRLEnv(scenario=make_scenario(n_env, cap=48, seed=5), precision=32, device=DEV)
+        env.reset()
+        env.init_step()
+        sm = PolicySampler(env, pol, chunk=32, seed=SEED, request_capacity=n_env, serve="queue", fused_actor=fused,
+                           actor_stream=stream)
+        assert sm.fused == fused and (sm.actor_stream is not None) == stream
+        sm.launch()
+        torch.cuda.synchronize()
+        cnt = int(sm.io["request_count"].item())
+        out.append((cnt, sm.io["request_env"][:cnt].cpu().numpy(), sm.io["policy_action"][:n_env].cpu().numpy(),
+                    sm.io["policy_ready"][:n_env].cpu().numpy(), int(sm.served.item())))
+    (c0, e0, a0, r0, s0), (c1, e1, a1, r1, s1) = out
+    assert c0 == c1 == n_env and np.array_equal(e0, e1)
+    assert s0 == s1 == n_env
+    assert np.array_equal(r0, r1) and (r0 == _lib.SIT_POLICY_READY).all()
+    err = np.abs(a0.astype(np.float64) - a1.astype(np.float64)).max()
+    print(f"PyTorch actor (fused ReLU epilogues, own stream) vs fused HIP actor: max |action| difference {err:.2e}")
+    assert err <= 1e-5
