@@ -569,8 +569,8 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       const int32_t q = xd.q[lane];
       live = q == kQLive;
       if (!live) {                     // no step in this row: the env waits for its action
-        if (uf & 8) *p_st = SIT_ST_NO_STEP;
-        if (uf & 4) *p_dn = 0;
+        if (uf & 8) out1(p_st, (uint32_t)SIT_ST_NO_STEP);
+        if (uf & 4) out1(p_dn, (uint8_t)0);
       } else {
         ++n_stepped;
       }
@@ -596,9 +596,9 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       const T rs = coll ? T(2000) : T(0);
       reward = r_nt_t + r_term_t + r_nto + r_o + r_snt + rs;
       const uint32_t status = ((bits_t | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
-      if (uf & 2) *p_rw = reward;
-      if (uf & 4) *p_dn = env_done ? 1 : 0;
-      if (uf & 8) *p_st = status;
+      if (uf & 2) out1(p_rw, reward);
+      if (uf & 4) out1(p_dn, (uint8_t)(env_done ? 1 : 0));
+      if (uf & 8) out1(p_st, status);
       sac = (f1 & kSfSac) != 0;
     }
     SY_MARK(6);
@@ -710,8 +710,8 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       if (TYPE == 0) {
         const T t4 = xd.t[4][lane];
         if (uf & 1) {                    // next_state columns 0-5 (MSRL_Env.py:426-437)
-          store2(p_ns, xd.t[0][lane], xd.t[1][lane]); store2(p_ns + 2, xd.t[2][lane], xd.t[3][lane]);
-          store2(p_ns + 4, t4, xd.t[5][lane]);
+          out2(p_ns, xd.t[0][lane], xd.t[1][lane]); out2(p_ns + 2, xd.t[2][lane], xd.t[3][lane]);
+          out2(p_ns + 4, t4, xd.t[5][lane]);
         }
         r_nt = xabs(t4) * c.inv_e_tol + (T(1) - dobst * c.inv_maxn) * T(0.01);
         const bool pred[6] = {(pbits & kPbArrive) != 0, (pbits & kPbHorizon) != 0, terrain, (fl & kSfMech) != 0,
@@ -730,10 +730,10 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
         r_nt_t = r_nt; r_term_t = r_term; bits_t = bits;
       } else {
         const T o3 = xd.o[3][lane];
-        if (uf & 1) { store2(p_ns, xd.o[0][lane], xd.o[1][lane]); store2(p_ns + 2, xd.o[2][lane], o3); }
+        if (uf & 1) { out2(p_ns, xd.o[0][lane], xd.o[1][lane]); out2(p_ns + 2, xd.o[2][lane], o3); }
         if (uf & 16) {                   // the IW action row: north, east, route angle, SAC_update
           const bool sac = (fl & kSfSac) != 0;
-          store2(p_ao, xd.iwn[lane], xd.iwe[lane]); store2(p_ao + 2, xd.ang[lane], sac ? T(1) : T(0));
+          out2(p_ao, xd.iwn[lane], xd.iwe[lane]); out2(p_ao + 2, xd.ang[lane], sac ? T(1) : T(0));
         }
         if (!stop)
           r_nt = T(0.1) - xabs(o3) * c.inv_e_tol * T(0.01) - (T(1) - dobst * c.inv_maxn) * T(0.01);

@@ -494,7 +494,7 @@ def test_f32_free_running_within_storage_bound():
     outcome differs (done, status, sampling event, waypoint index, route length, stop flags, episode
     step, sampler counter).  Gated: before divergence the next_state deviation (per-field floors) is
     within north_star's 1e-5 and below what plain float32 storage alone costs (the float32 handle keeps
-    its integrators as double-float values); at most 0.25 % of envs diverge.  Every divergence is attributed
+    its integrators as double-float values); at most 0.1 % of envs diverge (measured: none).  Every divergence is attributed
     (f32_drift.measure(attribute=True)): re-run in float64 from the float32 run's own pre-step state,
     the step takes the float32 decision (the state's float32 drift decided it), or, where it takes the
     float64 one, the flip is a hull-in-terrain decision whose exact (float64) predicate at the stored
@@ -535,7 +535,8 @@ def test_f32_free_running_within_storage_bound():
     # 38 envs diverged, max 9.95e-6; round 5: 9 envs, max 3.5e-6, profiles/r05_f32_flip_attribution.json)
     assert f32["next_state_max"] <= 1e-5
     assert f32["next_state_max"] <= s32["next_state_max"]
-    assert f32["envs_diverged"] <= 0.0025 * 4096
+    # round 6, every integrator double-float: 0 of 4 096 envs diverge (round 5: 8); a margin of 0.1 %
+    assert f32["envs_diverged"] <= 4
     # every real state field of both ships (pose, velocities, shaft speed, the PI / PID / LOS integrals, the
     # previous heading error) within the same 1e-5 before divergence.  (The heading PID integral, the time
     # integral of the heading error, follows the trajectory; it read 1.43e-5 until round 6 carried surge, sway,

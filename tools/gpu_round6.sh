@@ -88,7 +88,7 @@ g)
   tools/gpu_steps.sh \
     $T/tests 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sim.py -m gpu -v --timeout 300 --timeout-method thread \
       -k "launch_partition or equals_classic or f32_teacher_forced or synthetic_rollout or f32_rollout or free_running or knife or sim_" --- \
-    $T/ab 900 bash tools/ab_libs.sh 3 sac_maritime_ast_amd/libsit.so build_diag/libsit_$V.so build_diag/libsit_kb4.so ;;
+    $T/ab 900 bash tools/ab_libs.sh 3 sac_maritime_ast_amd/libsit.so build_diag/libsit_$V.so ;;
 h)
   V=${3:-nocompvel}
   tools/gpu_steps.sh \
