@@ -85,7 +85,10 @@ def parse():
     ap.add_argument("--c5-steps", type=int, default=32 * 16 * 16, help="timed steps of the C5 line")
     ap.add_argument("--c5-warmup", type=int, default=32 * 16 * 60, help="warm-up steps of the C5 line")
     ap.add_argument("--c5-groups", type=int, default=1, help="C5 line: stream groups (1 measured fastest)")
-    ap.add_argument("--c5-chunk", type=int, default=64, help="C5 line: env steps per launch")
+    ap.add_argument("--c5-chunk", type=int, default=80,
+                    help="C5 line: env steps per launch (an env that stops at a sampling event waits for the launch's "
+                         "end, so the idle share depends on the launch length against the events' spacing: K = 64 / 72 / "
+                         "76 / 80 / 84 / 96 measured 1.57 / 1.66 / 1.56 / 1.66 / 1.64 / 1.53e10, DESIGN.md §9)")
     ap.add_argument("--no-extra-lines", action="store_true",
                     help="rollout mode: skip the secondary lines (C3 in float64, C5 with the PyTorch-ROCm actor)")
     ap.add_argument("--trajectory-stride", type=int, default=0,
@@ -662,8 +665,8 @@ def main():
                            "roofline": r64["roofline"]}
         if not args.no_c5:
             at = argparse.Namespace(**vars(args))
-            at.mode, at.chunk, at.groups, at.serve, at.torch_actor, at.actor_stream = "policy", 64, 1, "queue", True, True
-            at.steps, at.warmup = 64 * 16 * 8, 64 * 16 * 15
+            at.mode, at.chunk, at.groups, at.serve, at.torch_actor, at.actor_stream = "policy", 80, 1, "queue", True, True
+            at.steps, at.warmup = 80 * 16 * 8, 80 * 16 * 12
             rt = bench_policy(at, rank, world, dev)
             extra["c5_torch_actor"] = {
                 "metric": "env-steps/sec, 65 536 policy-driven ships per GPU (config C5), PyTorch-ROCm actor",

@@ -12,9 +12,9 @@ P=${2:-a}
 O=gpurun_out/$T
 mkdir -p $O
 C3="--no-cpu-baseline --no-extra-lines --no-c5"
-C5="--no-cpu-baseline --mode policy --chunk 64 --groups 1 --steps 8192 --warmup 30720"
+C5="--no-cpu-baseline --mode policy --chunk 80 --groups 1 --steps 8192 --warmup 30720"
 F64="--no-cpu-baseline --no-extra-lines --no-c5 --precision 64 --chunk 10000 --steps 30000 --warmup 40000"
-TORCH="--no-cpu-baseline --mode policy --serve queue --torch-actor --actor-stream --groups 1 --chunk 64 --steps 8192 --warmup 15360"
+TORCH="--no-cpu-baseline --mode policy --serve queue --torch-actor --actor-stream --groups 1 --chunk 80 --steps 10240 --warmup 15360"
 RP="rocprofv3 --kernel-trace --stats -o run --output-format csv"
 case $P in
 a)
@@ -56,7 +56,7 @@ b)
     --n-env 32768 --mode rollout --round 6 --kernel "k_env_steps_sync<float, kSynth> (sit_sync.h)" \
     --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh --no-c5 (5 passes)"
   python3 tools/pmc_summary.py $O/pmc_c5 "k_env_steps_sync<float, 2" 8 > $O/pmc_summary_c5.json
-  python3 tools/make_profile_json.py $O/pmc_summary_c5.json $O/pmc_f32_policy.json --steps-per-launch 64 \
+  python3 tools/make_profile_json.py $O/pmc_summary_c5.json $O/pmc_f32_policy.json --steps-per-launch 80 \
     --n-env 32768 --mode policy --serve kernel --round 6 --kernel "k_env_steps_sync<float, kPolicy> (sit_sync.h), in-kernel serving" \
     --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh $C5 (5 passes; HIP-graph replays, 1 stream group)"
   python3 tools/pmc_summary.py $O/pmc_f64 "k_env_steps_sync<double" 1 > $O/pmc_summary_f64.json
@@ -64,7 +64,7 @@ b)
     --n-env 32768 --precision 64 --mode rollout --round 6 --kernel "k_env_steps_sync<double, kSynth> (sit_sync.h)" \
     --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh $F64 (5 passes)"
   python3 tools/pmc_summary.py $O/pmc_torch "k_env_steps_sync<float, 2" 8 > $O/pmc_summary_torch.json
-  python3 tools/make_profile_json.py $O/pmc_summary_torch.json $O/pmc_f32_policy_queue.json --steps-per-launch 64 \
+  python3 tools/make_profile_json.py $O/pmc_summary_torch.json $O/pmc_f32_policy_queue.json --steps-per-launch 80 \
     --n-env 32768 --mode policy --serve queue --round 6 --kernel "k_env_steps_sync<float, kPolicy> (sit_sync.h), request queue" \
     --source "rocprofv3 --kernel-trace --pmc, tools/pmc.sh $TORCH (5 passes; HIP-graph replays, actor on its own stream)"
   find $O -name "*.csv" -size +1M -delete
