@@ -569,8 +569,8 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       const int32_t q = xd.q[lane];
       live = q == kQLive;
       if (!live) {                     // no step in this row: the env waits for its action
-        if (uf & 8) out1(p_st, (uint32_t)SIT_ST_NO_STEP);
-        if (uf & 4) out1(p_dn, (uint8_t)0);
+        if (uf & 8) out1<T>(p_st, (uint32_t)SIT_ST_NO_STEP);
+        if (uf & 4) out1<T>(p_dn, (uint8_t)0);
       } else {
         ++n_stepped;
       }
@@ -596,9 +596,9 @@ __device__ __forceinline__ void sync_p(const KArgs<T>& a, const Consts<T>& cs, c
       const T rs = coll ? T(2000) : T(0);
       reward = r_nt_t + r_term_t + r_nto + r_o + r_snt + rs;
       const uint32_t status = ((bits_t | bo) & ~(kStopBit | kDoneBit)) | (coll ? SIT_ST_COLLISION : 0u);
-      if (uf & 2) out1(p_rw, reward);
-      if (uf & 4) out1(p_dn, (uint8_t)(env_done ? 1 : 0));
-      if (uf & 8) out1(p_st, status);
+      if (uf & 2) out1<T>(p_rw, reward);
+      if (uf & 4) out1<T>(p_dn, (uint8_t)(env_done ? 1 : 0));
+      if (uf & 8) out1<T>(p_st, status);
       sac = (f1 & kSfSac) != 0;
     }
     SY_MARK(6);
