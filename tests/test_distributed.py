@@ -179,3 +179,52 @@ def test_trajectory_gather_two_ranks(tmp_path):
     path = str(tmp_path / "result_traj.txt")
     mp.spawn(_traj_worker, args=(2, _free_port(), path), nprocs=2, join=True)
     assert open(path).read() == "ok"
+
+
+def _subgroup_worker(rank, world, port, result_path):
+    """The gathers inside a process subgroup ({1, 2} of a world of 3): ranks, world size and the learner
+    count within the group, while torch.distributed's point-to-point ops take GLOBAL peer ranks
+    (shard._peer maps them).  Group rank 0 (global rank 1) is the learner and must receive global rank
+    2's records and trajectory rows; global rank 0 is not a member and moves nothing."""
+    from sac_maritime_ast_amd.shard import TrajectoryGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        grp = dist.new_group([1, 2])
+        if rank in (1, 2):
+            # replay records: 3 + rank valid rows, tagged with the global rank
+            tr = torch.zeros((16, 24), dtype=torch.float64)
+            n = 3 + rank
+            tr[:n, 0] = float(rank)
+            tr[:n, 23] = torch.arange(n, dtype=torch.float64)
+            g = TransitionGather(16, 24, torch.float64, "cpu", 2, group=grp, dst=0)
+            g(tr, torch.tensor([n], dtype=torch.int32))
+            # trajectory rows: value = 1000 * global rank + step
+            k, n_env, stride = 9, 4, 2
+            steps = torch.arange(k, dtype=torch.float64)[:, None]
+            out = {"next_state": (1000.0 * rank + steps)[:, :, None].expand(k, n_env, 10).contiguous(),
+                   "reward": (1000.0 * rank + steps).expand(k, n_env).contiguous(),
+                   "done": torch.zeros((k, n_env), dtype=torch.uint8),
+                   "status": torch.full((k, n_env), rank, dtype=torch.int32)}
+            tg = TrajectoryGather(k, n_env, stride, torch.float64, "cpu", 2, group=grp, dst=0)
+            tg.start(out)
+            tg.wait()
+            if rank == 1:
+                rec = g.records()
+                assert rec.shape[0] == (3 + 1) + (3 + 2)
+                assert (rec[:4, 0] == 1).all() and (rec[4:, 0] == 2).all()
+                rw = tg.gathered("reward")                      # [2, rows, n_env]: group ranks 0, 1
+                want = torch.arange(0, k, stride, dtype=torch.float64)[:, None].expand(-1, n_env)
+                assert torch.equal(rw[0], 1000.0 + want) and torch.equal(rw[1], 2000.0 + want)
+                assert (tg.gathered("status")[1] == 2).all()
+                with open(result_path, "w") as f:
+                    f.write("ok")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gathers_in_a_process_subgroup(tmp_path):
+    path = str(tmp_path / "result_group.txt")
+    mp.spawn(_subgroup_worker, args=(3, _free_port(), path), nprocs=3, join=True)
+    assert open(path).read() == "ok"

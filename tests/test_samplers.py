@@ -105,3 +105,21 @@ def test_pack_actor_weights_in_place_equals_fresh_pack():
     w2t = out[H * _lib.SIT_OBS_DIM + H:H * _lib.SIT_OBS_DIM + H + H * H].view(H, H)
     assert torch.equal(w2t, l2.weight.detach().t())
     assert pack_actor_weights(GaussianPolicy(hidden=(64, 64))) is None   # other architectures: generic path
+
+
+def test_pack_actor_weights_rejects_a_wrong_out_buffer():
+    """pack_actor_weights(out=...) checks the buffer before writing: its size, dtype and contiguity
+    (a larger buffer was partly written with a stale tail, a wrong dtype failed late)."""
+    import pytest
+
+    from sac_maritime_ast_amd import _lib
+    from sac_maritime_ast_amd.samplers import _trunk, pack_actor_weights
+    pol = GaussianPolicy()
+    n = _lib.SIT_ACTOR_WEIGHTS
+    for bad in (torch.zeros(n + 1), torch.zeros(n - 1), torch.zeros(n, dtype=torch.float64), torch.zeros(2 * n)[::2]):
+        with pytest.raises(ValueError):
+            pack_actor_weights(pol, out=bad)
+    # the PyTorch actor's trunk with fused ReLU epilogues is the network itself
+    x = torch.randn(33, 10, dtype=torch.float64)
+    p64 = GaussianPolicy().double()
+    assert torch.equal(_trunk(p64.net, x), p64.net(x))
