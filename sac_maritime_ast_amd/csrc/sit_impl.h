@@ -354,7 +354,7 @@ __device__ __forceinline__ double angle_or_nan(bool has, double a) {
 //           admission kernel after the launch queues its request, and the next launch consumes
 //           the action the policy wrote for it)
 // ---------------------------------------------------------------------------------------
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC) || defined(SIT_DIAG_PLACE)
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC) || defined(SIT_DIAG_SERVE) || defined(SIT_DIAG_PLACE)
 // Diagnostic builds only (tools/diag_paths.py, tools/diag_sync.py): [type][0..15] predicate path
 // statistics, [type][16..23] shader-clock cycles per step phase (wave lane 0); SIT_DIAG_SYNC: cycles
 // per role and segment of k_env_steps_sync (sit_sync.h).  The counters are per translation unit:

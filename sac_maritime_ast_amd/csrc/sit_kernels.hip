@@ -45,7 +45,7 @@ int launch_selftest_f32tu(int op, int n, const double* a, const double* b, doubl
 // =======================================================================================
 extern "C" {
 
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC)
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC) || defined(SIT_DIAG_SERVE)
 #ifdef SIT_DIAG_PHASES
 int sit_diag_read_waves(unsigned long long* out, int n) {   // [n][4], diagnostic builds only
   if (hipDeviceSynchronize() != hipSuccess) return -1;

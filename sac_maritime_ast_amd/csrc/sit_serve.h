@@ -132,6 +132,11 @@ __host__ __device__ constexpr size_t serve_lds_bytes(size_t map_bytes) {
   return serve_pub_offset<T>(map_bytes) + serve_align(sizeof(ServePub));
 }
 
+// SIT_DIAG_SERVE (diagnostic builds only, tools/diag_serve.py; not with SIT_DIAG_SYNC): per pass, lane 0 of
+// wave 0 counts the pass in g_sit_diag[1][R / 4] and sums its duration in s_memtime / s_memrealtime (100 MHz)
+// ticks into g_sit_diag[1][8] / [1][9].  (Stamps between the pass's phases were tried: their waits serialize
+// the W2^T stream and tripled the pass, so only the whole pass is timed.)
+
 // One pass of the actor over published rows [row0, row0 + kServeRows) by the block's 256 threads:
 // layer 1 (thread j = hidden unit j), layer 2 split over K (wave q sums inputs [64 q, 64 q + 64) for
 // all 256 units, lane l owning units 4l..4l+3: one coalesced float4 of W2^T per k, the activations
@@ -146,6 +151,9 @@ __device__ __forceinline__ void serve_pass(const float* __restrict__ w, const Se
   static_assert(R % 2 == 0 && R <= kServeRows, "pass rows");
   constexpr int H = kActorHidden, KB = kServeKB;
   const int j = threadIdx.x, q = j >> 6, l = j & 63;
+#ifdef SIT_DIAG_SERVE
+  const unsigned long long sv_m0 = __builtin_amdgcn_s_memtime(), sv_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // layer 1: h1 = relu(W1 obs + b1), one row pair at a time (unrolled over all rows, the compiler
   // held every row's observation in registers at once)
 #pragma unroll 1
@@ -245,6 +253,13 @@ __device__ __forceinline__ void serve_pass(const float* __restrict__ w, const Se
     if (c == 0) W.head[pr] = sum + w[kActorB3 + o];
   }
   __syncthreads();
+#ifdef SIT_DIAG_SERVE
+  if (j == 0) {
+    atomicAdd(&g_sit_diag[1][R / 4], 1ull);
+    atomicAdd(&g_sit_diag[1][8], __builtin_amdgcn_s_memtime() - sv_m0);
+    atomicAdd(&g_sit_diag[1][9], __builtin_amdgcn_s_memrealtime() - sv_r0);
+  }
+#endif
 }
 
 // The block's waiting envs served: every pass of kServeRows rows, then each row's head and the

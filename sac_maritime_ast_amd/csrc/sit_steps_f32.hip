@@ -22,7 +22,7 @@ int sit_launch_selftest_f32tu(int op, int n, const double* a, const double* b, d
   return launch_selftest(op, n, a, b, out, (hipStream_t)stream);
 }
 
-#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC) || defined(SIT_DIAG_PLACE)
+#if defined(SIT_DIAG_PATHS) || defined(SIT_DIAG_PHASES) || defined(SIT_DIAG_SYNC) || defined(SIT_DIAG_SERVE) || defined(SIT_DIAG_PLACE)
 // diagnostic builds only: this TU's counters (the float32 step kernels')
 extern "C" int sit_diag_read_f32(unsigned long long* out, int reset) { return diag_read_impl(out, reset); }
 #endif
